@@ -1,0 +1,593 @@
+#!/usr/bin/env python
+"""Golden-vector generator: runs the REFERENCE smcdet (imported from
+/root/reference, CPU, float32 default dtype) and records inputs, every random
+draw it makes, and its outputs as small .npz fixtures under tests/golden/.
+
+Test infrastructure only.  It runs in the build container (where the
+reference is mounted read-only); the GPU box only ever sees the .npz/.json
+files it wrote.  Nothing here is imported by the product package.
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py fixtures
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py stats   # slow
+
+Recording: torch.rand and torch.distributions.Multinomial.sample are wrapped
+so that every draw the reference makes (prior sampling, truncated-normal
+proposals, accept uniforms, systematic-resampling offsets, component masks)
+is captured in call order.  The reference's own RNG stream is unchanged.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REF)
+
+from smcdet.distributions import TruncatedDiagonalMVN, TruncatedPareto  # noqa: E402
+from smcdet.images import ImageModel, M71ImageModel, generate_images  # noqa: E402
+from smcdet.kernel import SingleComponentMH  # noqa: E402
+from smcdet.prior import M71Prior, ParetoStarPrior  # noqa: E402
+from smcdet.sampler import SMCsampler  # noqa: E402
+
+# M71 parameters (notebooks/smc.ipynb cell 2; full precision per SURVEY §8a)
+M71 = dict(
+    flux_alpha=0.21411753249015655,
+    flux_lower=0.06291294097900389,
+    flux_upper=1804.6791992187502,
+    flux_detection_threshold=0.25165176391601557,
+    counts_rate=0.030264640226960182,
+    background=104.1486587524414,
+    adu_per_nmgy=241.02658081054688,
+    psf_params=[1.107237458229065, 2.0800251960754395, 2.3254318237304688,
+                5.240590572357178, 0.7346734404563904, 0.5114791393280029],
+    psf_radius=8,
+    noise_additive=1.0000007072408224e-10,
+    noise_multiplicative=1.936462640762329,
+)
+# experiments/basic/generate_images.py:26-60
+BASIC_PSF_STDEV = 0.93
+BASIC_BACKGROUND = 200.0
+_psf_max = 1 / (2 * np.pi * BASIC_PSF_STDEV ** 2)
+BASIC_FLUX_SCALE = 5 * np.sqrt(BASIC_BACKGROUND) / _psf_max
+BASIC_FLUX_ALPHA = (-np.log(1 - 0.99)) / (
+    np.log(50 * np.sqrt(BASIC_BACKGROUND) / _psf_max) - np.log(BASIC_FLUX_SCALE))
+
+
+class Recorder:
+    """Wraps torch.rand / Multinomial.sample / Tensor.multinomial; records draws."""
+
+    def __init__(self):
+        self.draws = []  # list of (kind, np.ndarray)
+
+    def __enter__(self):
+        rec = self
+        self._rand = torch.rand
+        self._ms = torch.distributions.Multinomial.sample
+        self._tm = torch.Tensor.multinomial
+
+        def rand(*a, **k):
+            out = rec._rand(*a, **k)
+            rec.draws.append(("rand", out.detach().cpu().numpy().copy()))
+            return out
+
+        def ms(self_, sample_shape=torch.Size()):
+            out = rec._ms(self_, sample_shape)
+            rec.draws.append(("mask", out.detach().cpu().numpy().copy()))
+            return out
+
+        def tm(self_, *a, **k):
+            out = rec._tm(self_, *a, **k)
+            rec.draws.append(("multinomial", out.detach().cpu().numpy().copy()))
+            return out
+
+        torch.rand = rand
+        torch.distributions.Multinomial.sample = ms
+        torch.Tensor.multinomial = tm
+        return self
+
+    def __exit__(self, *exc):
+        torch.rand = self._rand
+        torch.distributions.Multinomial.sample = self._ms
+        torch.Tensor.multinomial = self._tm
+        return False
+
+
+def m71_model(H, psf_params=None):
+    p = M71
+    return M71ImageModel(
+        image_height=H, image_width=H, background=p["background"],
+        psf_radius=p["psf_radius"], adu_per_nmgy=p["adu_per_nmgy"],
+        psf_params=torch.tensor(p["psf_params"] if psf_params is None else psf_params),
+        noise_additive=p["noise_additive"],
+        noise_multiplicative=p["noise_multiplicative"])
+
+
+def m71_prior(H, smin, smax, pad=4, counts_rate=None, flux_lower=None):
+    p = M71
+    return M71Prior(
+        min_objects=smin, max_objects=smax,
+        counts_rate=p["counts_rate"] if counts_rate is None else counts_rate,
+        image_height=H, image_width=H, flux_alpha=p["flux_alpha"],
+        flux_lower=p["flux_lower"] if flux_lower is None else flux_lower,
+        flux_upper=p["flux_upper"], pad=pad)
+
+
+def basic_model(H):
+    return ImageModel(image_height=H, image_width=H, psf_radius=8,
+                      psf_stdev=BASIC_PSF_STDEV, background=BASIC_BACKGROUND)
+
+
+def basic_prior(H, smin, smax, pad=2):
+    return ParetoStarPrior(min_objects=smin, max_objects=smax, image_height=H,
+                           image_width=H, flux_scale=BASIC_FLUX_SCALE * 0.9,
+                           flux_alpha=BASIC_FLUX_ALPHA, pad=pad)
+
+
+def m71_truth_image(H, seed, counts_rate=None, max_sources=None):
+    """generate_images() with a Poisson-count M71 truth prior (as
+    experiments/m71synthetic/generate_images.py:27-67)."""
+    torch.manual_seed(seed)
+    tp = m71_prior(H, 0, 100, pad=4, counts_rate=counts_rate,
+                   flux_lower=M71["flux_detection_threshold"])
+    while True:
+        res = generate_images(tp, m71_model(H), M71["flux_detection_threshold"], 0, H, 1)
+        if max_sources is None or int(res[0][0]) <= max_sources:
+            return res
+
+
+def basic_truth_image(H, seed):
+    """experiments/basic/generate_images.py:26-94 (one image)."""
+    torch.manual_seed(seed)
+    tp = basic_prior(H, 0, 3)
+    return generate_images(tp, basic_model(H), BASIC_FLUX_SCALE, 0, H, 1)
+
+
+def sampler_for(image, tile_dim, prior, model, mh, N, method="systematic",
+                max_iters=100):
+    return SMCsampler(image=image, tile_dim=tile_dim, Prior=prior, ImageModel=model,
+                      MutationKernel=mh, num_catalogs=N, ess_threshold_prop=0.5,
+                      resample_method=method,
+                      flux_detection_threshold=M71["flux_detection_threshold"],
+                      max_smc_iters=max_iters, print_every=10 ** 9)
+
+
+def np32(t):
+    return t.detach().cpu().numpy().astype(np.float32)
+
+
+def save(name, **arrs):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrs.items()})
+    print("wrote", path, sum(np.asarray(v).nbytes for v in arrs.values()), "bytes raw")
+
+
+# ----------------------------------------------------------------------------
+def gen_psf():
+    out = {}
+    for H in (8, 16, 32):
+        pts = [(H / 2 + 0.3, H / 2 + 0.7), (3.0, 5.0), (-3.2, 2.5), (H - 0.01, 0.01),
+               (H + 3.9, -3.9), (0.5, 0.5), (-0.25, H - 0.75), (1.999, 2.001)]
+        locs = torch.tensor(pts, dtype=torch.float32).reshape(1, 1, 2, 4, 2)
+        m = m71_model(H)
+        out[f"m71_H{H}_locs"] = np32(locs)
+        out[f"m71_H{H}_psf"] = np32(m.psf(locs))
+        if H == 16:
+            b = basic_model(H)
+            out[f"basic_H{H}_psf"] = np32(b.psf(locs))
+    m = m71_model(8)
+    out["m71_norm_const_f32"] = np.float32(m.psf_normalizing_constant.item())
+    r = torch.linspace(0, 12, 97)
+    out["m71_r"] = np32(r)
+    out["m71_unnorm"] = np32(m._compute_unnormalized_psf(r))
+    out["m71_norm"] = np32(m._compute_normalized_psf(r))
+    out["basic_norm"] = np32(basic_model(8)._compute_normalized_psf(r))
+    save("psf.npz", **out)
+
+
+def gen_loglik():
+    out = {}
+    # M71 single tiles, prior catalogs around a synthetic truth image
+    for H, S, N, seed in ((8, 10, 64, 1), (32, 10, 32, 2), (16, 3, 48, 3)):
+        res = m71_truth_image(H, seed, counts_rate=M71["counts_rate"] if H == 8 else 0.003125)
+        img = res[-1][0]
+        torch.manual_seed(100 + seed)
+        pr = m71_prior(H, S, S)
+        counts, locs, fluxes = pr.sample(num_tiles_per_side=1, stratify_by_count=True,
+                                         num_catalogs_per_count=N)
+        # include a few states near a posterior mode: copy truth into particle 0
+        tl, tf = res[1][0], res[2][0]
+        k = min(S, tl.shape[0])
+        locs[0, 0, 0, :k] = tl[:k]
+        fluxes[0, 0, 0, :k] = tf[:k].clamp(min=pr.flux_lower)
+        m = m71_model(H)
+        tiled = img.unsqueeze(0).unsqueeze(0)
+        key = f"m71_H{H}_S{S}"
+        out[key + "_image"] = np32(img)
+        out[key + "_locs"] = np32(locs)
+        out[key + "_fluxes"] = np32(fluxes)
+        out[key + "_counts"] = np32(counts)
+        out[key + "_loglik"] = np32(m.loglikelihood(tiled, locs, fluxes))
+        out[key + "_logprior"] = np32(pr.log_prob(counts, locs, fluxes))
+        # float64 reference evaluation of the same states
+        torch.set_default_dtype(torch.float64)
+        try:
+            m64 = m71_model(H)
+            ll64 = m64.loglikelihood(tiled.double(), locs.double(), fluxes.double())
+            out[key + "_loglik_f64"] = ll64.numpy()
+        finally:
+            torch.set_default_dtype(torch.float32)
+    # multi-tile (2x2 tiles of 8x8 from a 16x16 image): checks unfold/tiling
+    res = m71_truth_image(16, 7)
+    img = res[-1][0]
+    torch.manual_seed(107)
+    pr = m71_prior(8, 4, 4)
+    counts, locs, fluxes = pr.sample(num_tiles_per_side=2, stratify_by_count=True,
+                                     num_catalogs_per_count=16)
+    m = m71_model(8)
+    tiled = img.unfold(0, 8, 8).unfold(1, 8, 8)
+    out["m71_tiles_image"] = np32(img)
+    out["m71_tiles_locs"] = np32(locs)
+    out["m71_tiles_fluxes"] = np32(fluxes)
+    out["m71_tiles_loglik"] = np32(m.loglikelihood(tiled, locs, fluxes))
+    # Poisson (basic) model
+    res = basic_truth_image(16, 11)
+    img = res[-1][0]
+    torch.manual_seed(111)
+    pr = basic_prior(16, 3, 3)
+    counts, locs, fluxes = pr.sample(num_tiles_per_side=1, stratify_by_count=True,
+                                     num_catalogs_per_count=64)
+    b = basic_model(16)
+    tiled = img.unsqueeze(0).unsqueeze(0)
+    out["basic_H16_S3_image"] = np32(img)
+    out["basic_H16_S3_locs"] = np32(locs)
+    out["basic_H16_S3_fluxes"] = np32(fluxes)
+    out["basic_H16_S3_counts"] = np32(counts)
+    out["basic_H16_S3_loglik"] = np32(b.loglikelihood(tiled, locs, fluxes))
+    out["basic_H16_S3_logprior"] = np32(pr.log_prob(counts, locs, fluxes))
+    # Poisson model with the rate > 5e4 (normal-approximation) branch exercised
+    locs2 = locs.clone()
+    fl2 = fluxes.clone()
+    fl2[0, 0, :8, 0] = torch.linspace(2e5, 2e6, 8)
+    locs2[0, 0, :8, 0] = torch.tensor([7.5, 8.5])
+    img2 = img.clone()
+    img2[7:10, 7:10] += 60000.0
+    out["basic_bright_image"] = np32(img2)
+    out["basic_bright_locs"] = np32(locs2)
+    out["basic_bright_fluxes"] = np32(fl2)
+    out["basic_bright_loglik"] = np32(b.loglikelihood(img2.unsqueeze(0).unsqueeze(0), locs2, fl2))
+    save("loglik.npz", **out)
+
+
+def gen_prior():
+    out = {}
+    torch.manual_seed(21)
+    # counts varying 0..S to exercise the count mask (min < max)
+    pr = m71_prior(8, 0, 12, counts_rate=0.01)
+    with Recorder() as rec:
+        counts, locs, fluxes = pr.sample(num_catalogs=40, num_tiles_per_side=2)
+    out["m71_counts"] = np32(counts)
+    out["m71_locs"] = np32(locs)
+    out["m71_fluxes"] = np32(fluxes)
+    out["m71_logprior"] = np32(pr.log_prob(counts, locs, fluxes))
+    # stratified sampling draws (initialize() path, prior.py:47-64)
+    torch.manual_seed(22)
+    pr = m71_prior(8, 3, 5)
+    with Recorder() as rec:
+        counts, locs, fluxes = pr.sample(num_tiles_per_side=2, stratify_by_count=True,
+                                         num_catalogs_per_count=8)
+    assert [k for k, _ in rec.draws] == ["rand", "rand"]
+    out["m71_strat_uloc"] = rec.draws[0][1]
+    out["m71_strat_uflux"] = rec.draws[1][1]
+    out["m71_strat_counts"] = np32(counts)
+    out["m71_strat_locs"] = np32(locs)
+    out["m71_strat_fluxes"] = np32(fluxes)
+    out["m71_strat_logprior"] = np32(pr.log_prob(counts, locs, fluxes))
+    torch.manual_seed(23)
+    pr = basic_prior(16, 3, 3)
+    with Recorder() as rec:
+        counts, locs, fluxes = pr.sample(num_tiles_per_side=1, stratify_by_count=True,
+                                         num_catalogs_per_count=32)
+    out["basic_counts"] = np32(counts)
+    out["basic_locs"] = np32(locs)
+    out["basic_fluxes"] = np32(fluxes)
+    out["basic_logprior"] = np32(pr.log_prob(counts, locs, fluxes))
+    save("prior.npz", **out)
+
+
+def gen_distributions():
+    out = {}
+    torch.manual_seed(31)
+    # truncated normal: loc-like (sigma 0.1, box [-4, 36]) and flux-like
+    mu_l = torch.cat([torch.rand(200, 2) * 40 - 4, torch.tensor([[-4.0, 36.0], [-3.95, 35.97]])])
+    mu_f = torch.cat([torch.rand(100) * 3, torch.rand(100) * 1800,
+                      torch.tensor([0.06291294097900389, 1804.6791992187502])])
+    for name, mu, sig, lb, ub in (
+            ("loc", mu_l, torch.tensor(0.1), -4 * torch.ones(2), torch.tensor([36.0, 36.0])),
+            ("flux", mu_f, 2.5 * torch.ones(1), M71["flux_lower"] * torch.ones(1),
+             M71["flux_upper"] * torch.ones(1))):
+        d = TruncatedDiagonalMVN(mu, sig, lb, ub)
+        with Recorder() as rec:
+            x = d.sample()
+        out[name + "_mu"] = np32(mu)
+        out[name + "_u"] = rec.draws[0][1]
+        out[name + "_x"] = np32(x)
+        out[name + "_logprob_x"] = np32(d.log_prob(x))
+        out[name + "_logZ"] = np32(d.log_prob_in_box)
+    tp = TruncatedPareto(M71["flux_alpha"], M71["flux_lower"], M71["flux_upper"])
+    with Recorder() as rec:
+        f = tp.sample([500])
+    out["tpareto_u"] = rec.draws[0][1]
+    out["tpareto_x"] = np32(f)
+    out["tpareto_logprob"] = np32(tp.log_prob(f))
+    save("distributions.npz", **out)
+
+
+def run_mh_recorded(image, tile_dim, prior, model, mh, N, tau, seed):
+    """Runs SingleComponentMH.run once with recorded draws and proposals."""
+    torch.manual_seed(seed)
+    s = sampler_for(image, tile_dim, prior, model, mh, N)
+    s.initialize()
+    nt = s.num_tiles_per_side
+    temperature = torch.full((nt, nt), float(tau))
+    proposals = []
+    orig = s.log_target
+
+    def log_target(data, counts, locs, fluxes, temperature):
+        v = orig(data, counts, locs, fluxes, temperature)
+        proposals.append((np32(locs), np32(fluxes), np32(v)))
+        return v
+
+    locs0, fluxes0 = s.locs.clone(), s.fluxes.clone()
+    with Recorder() as rec:
+        locs1, fluxes1, acc = mh.run(s.tiled_image, s.counts, s.locs, s.fluxes,
+                                     temperature, log_target)
+    K = mh.num_iters
+    kinds = [k for k, _ in rec.draws]
+    assert kinds == ["mask", "rand", "rand", "rand"] * K, kinds[:8]
+    masks = np.stack([rec.draws[4 * i][1] for i in range(K)])
+    uloc = np.stack([rec.draws[4 * i + 1][1] for i in range(K)])
+    uflux = np.stack([rec.draws[4 * i + 2][1] for i in range(K)])
+    uacc = np.stack([rec.draws[4 * i + 3][1] for i in range(K)])
+    comp = masks.argmax(-1).astype(np.int32)  # [K,nt,nt,N]
+    j = comp[..., None]
+    uloc_sel = np.take_along_axis(uloc, j[..., None].repeat(2, -1)[..., None, :].reshape(
+        *j.shape[:-1], 1, 2), axis=-2)[..., 0, :]
+    uflux_sel = np.take_along_axis(uflux, j, axis=-1)[..., 0]
+    # log_target call order: iter0 numerator, iter0 denominator, then one numerator per iter
+    prop_locs = np.stack([proposals[0][0]] + [proposals[i][0] for i in range(2, K + 1)])
+    prop_fluxes = np.stack([proposals[0][1]] + [proposals[i][1] for i in range(2, K + 1)])
+    prop_lt = np.stack([proposals[0][2]] + [proposals[i][2] for i in range(2, K + 1)])
+    return dict(image=np32(s.image), counts=np32(s.counts), locs0=np32(locs0),
+                fluxes0=np32(fluxes0), tau=np.float32(tau), comp=comp,
+                uloc=uloc_sel.astype(np.float32), uflux=uflux_sel.astype(np.float32),
+                uacc=uacc.astype(np.float32), locs1=np32(locs1), fluxes1=np32(fluxes1),
+                acc=np32(acc), prop_locs=prop_locs, prop_fluxes=prop_fluxes,
+                prop_logtarget=prop_lt, init_logtarget=proposals[1][2],
+                locs_min=np32(mh.locs_min), locs_max=np32(mh.locs_max))
+
+
+def gen_mh():
+    # M71 8x8, S=4, N=32, K=20
+    res = m71_truth_image(8, 41)
+    mh = SingleComponentMH(20, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    d = run_mh_recorded(res[-1][0], 8, m71_prior(8, 4, 4), m71_model(8), mh, 32, 0.3, 141)
+    save("mh_m71_8x8.npz", **d)
+    # M71 32x32 (C2 geometry), S=10, N=8, K=10
+    res = m71_truth_image(32, 42, counts_rate=0.003125, max_sources=10)
+    mh = SingleComponentMH(10, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    d = run_mh_recorded(res[-1][0], 32, m71_prior(32, 10, 10), m71_model(32), mh, 8, 0.05, 142)
+    save("mh_m71_32x32.npz", **d)
+    # 2x2 tiles of 8x8 at tau=1 (multi-tile indexing)
+    res = m71_truth_image(16, 43)
+    mh = SingleComponentMH(10, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    d = run_mh_recorded(res[-1][0], 8, m71_prior(8, 3, 3), m71_model(8), mh, 8, 1.0, 143)
+    save("mh_m71_tiles.npz", **d)
+    # basic Poisson model (config 1 family) 16x16, S=3, N=32, K=20
+    res = basic_truth_image(16, 44)
+    pr = basic_prior(16, 3, 3)
+    mh = SingleComponentMH(20, 0.1, 100, pr.flux_scale, 1e6)
+    d = run_mh_recorded(res[-1][0], 16, pr, basic_model(16), mh, 32, 0.5, 144)
+    save("mh_basic_16x16.npz", **d)
+
+
+def gen_smc_steps():
+    out = {}
+    # temper: loglik vectors from prior states of a 32x32 tile, several tau
+    res = m71_truth_image(32, 51, counts_rate=0.003125, max_sources=10)
+    img = res[-1][0]
+    mh = SingleComponentMH(1, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    torch.manual_seed(151)
+    s = sampler_for(img, 16, m71_prior(16, 5, 5), m71_model(16), mh, 512)
+    s.initialize()
+    lls = s.loglik.clone()  # [2,2,512]
+    taus = torch.tensor([[0.0, 0.3], [0.999, 0.9999]])
+    s.temperature = taus.clone()
+    s.temper()
+    out["temper_loglik"] = np32(lls)
+    out["temper_tau_in"] = np32(taus)
+    out["temper_tau_out"] = np32(s.temperature)
+    out["temper_delta"] = (s.temperature.double() - taus.double()).numpy()
+    out["temper_rho_N"] = np.float64(s.ess_threshold)
+    # update_weights
+    s.log_normalizing_constant = torch.tensor([[-3.0, 0.0], [10.0, -1000.0]])
+    lz0 = s.log_normalizing_constant.clone()
+    s.update_weights()
+    out["weights_logZ_in"] = np32(lz0)
+    out["weights_W"] = np32(s.weights)
+    out["weights_ess"] = np32(s.ess)
+    out["weights_logZ"] = np32(s.log_normalizing_constant)
+    # systematic resampling with recorded offset
+    torch.manual_seed(152)
+    s.resample_method = "systematic"
+    W = s.weights.clone()
+    with Recorder() as rec:
+        s_counts0 = s.counts.clone()
+        s.resample()
+    U = rec.draws[0][1]
+    seq = torch.arange(512)
+    u = (seq + torch.tensor(U).unsqueeze(-1)) / 512
+    bins = W.cumsum(-1)
+    idx = torch.stack([torch.stack([torch.bucketize(u[h, w], bins[h, w]) for w in range(2)])
+                       for h in range(2)]).clamp(0, 511)
+    out["resample_W"] = np32(W)
+    out["resample_U"] = U
+    out["resample_idx"] = idx.numpy().astype(np.int64)
+    out["resample_counts_in"] = np32(s_counts0)
+    # systematic on handcrafted weights (zeros, a single spike, ties)
+    Wh = torch.zeros(3, 1, 64)
+    Wh[0, 0, 5] = 1.0
+    Wh[1, 0] = 1.0 / 64
+    Wh[2, 0, ::8] = 0.125
+    Uh = torch.tensor([[0.0], [0.5], [0.999999]])
+    uh = (torch.arange(64) + Uh.unsqueeze(-1)) / 64
+    bh = Wh.cumsum(-1)
+    idxh = torch.stack([torch.bucketize(uh[i, 0], bh[i, 0]) for i in range(3)]).clamp(0, 63)
+    out["resample_hand_W"] = np32(Wh)
+    out["resample_hand_U"] = np32(Uh)
+    out["resample_hand_idx"] = idxh.numpy().astype(np.int64)[:, None, :]
+    # prune
+    torch.manual_seed(153)
+    locs = torch.rand(2, 2, 64, 6, 2) * 24 - 4
+    locs[0, 0, 0, 0] = torch.tensor([0.0, 3.0])
+    locs[0, 0, 0, 1] = torch.tensor([16.0, 3.0])
+    fl = torch.rand(2, 2, 64, 6) * 0.6
+    pc, pl, pf = s.prune(locs, fl)
+    out["prune_locs"] = np32(locs)
+    out["prune_fluxes"] = np32(fl)
+    out["prune_counts"] = pc.numpy().astype(np.int64)
+    out["prune_out_locs"] = np32(pl)
+    out["prune_out_fluxes"] = np32(pf)
+    out["prune_tile_dim"] = np.int64(16)
+    out["prune_threshold"] = np.float64(M71["flux_detection_threshold"])
+    save("smc_steps.npz", **out)
+
+
+def run_smc_recorded(image, tile_dim, prior, model, mh, N, method, seed, max_iters):
+    torch.manual_seed(seed)
+    s = sampler_for(image, tile_dim, prior, model, mh, N, method=method, max_iters=max_iters)
+    trace = {"tau": [], "logZ": [], "ess": [], "acc": []}
+    orig_uw = s.update_weights
+
+    def uw():
+        orig_uw()
+        trace["tau"].append(np32(s.temperature))
+        trace["logZ"].append(np32(s.log_normalizing_constant))
+        trace["ess"].append(np32(s.ess))
+        trace["acc"].append(np32(getattr(s, "mutation_acc_rates", torch.zeros_like(s.temperature))))
+
+    s.update_weights = uw
+    import contextlib
+    import io
+    with Recorder() as rec, contextlib.redirect_stdout(io.StringIO()):
+        s.run()
+    draws = {f"draw_{i:04d}_{k}": v for i, (k, v) in enumerate(rec.draws)}
+    return s, trace, draws
+
+
+def gen_smc_replay():
+    # end-to-end replay: M71 8x8 tile, S=4, N=64, K=5, systematic
+    res = m71_truth_image(8, 61)
+    mh = SingleComponentMH(5, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    s, trace, draws = run_smc_recorded(res[-1][0], 8, m71_prior(8, 4, 4), m71_model(8), mh,
+                                       64, "systematic", 161, 100)
+    out = dict(image=np32(s.image), tile_dim=np.int64(8), N=np.int64(64), K=np.int64(5),
+               S=np.int64(4), iters=np.int64(s.iter), counts=np32(s.counts), locs=np32(s.locs),
+               fluxes=np32(s.fluxes), weights=np32(s.weights), ess=np32(s.ess),
+               logZ=np32(s.log_normalizing_constant), temperature=np32(s.temperature),
+               acc=np32(s.mutation_acc_rates), pruned_counts=s.pruned_counts.numpy(),
+               pruned_locs=np32(s.pruned_locs), pruned_fluxes=np32(s.pruned_fluxes),
+               trace_tau=np.stack(trace["tau"]), trace_logZ=np.stack(trace["logZ"]),
+               trace_ess=np.stack(trace["ess"]), **draws)
+    save("smc_replay_m71_8x8.npz", **out)
+    # 2x2 tiles of 8x8 (lockstep stop across tiles), S=3, N=32, K=4
+    res = m71_truth_image(16, 62)
+    mh = SingleComponentMH(4, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    s, trace, draws = run_smc_recorded(res[-1][0], 8, m71_prior(8, 3, 3), m71_model(8), mh,
+                                       32, "systematic", 162, 100)
+    out = dict(image=np32(s.image), tile_dim=np.int64(8), N=np.int64(32), K=np.int64(4),
+               S=np.int64(3), iters=np.int64(s.iter), counts=np32(s.counts), locs=np32(s.locs),
+               fluxes=np32(s.fluxes), weights=np32(s.weights), ess=np32(s.ess),
+               logZ=np32(s.log_normalizing_constant), temperature=np32(s.temperature),
+               acc=np32(s.mutation_acc_rates), pruned_counts=s.pruned_counts.numpy(),
+               pruned_locs=np32(s.pruned_locs), pruned_fluxes=np32(s.pruned_fluxes),
+               trace_tau=np.stack(trace["tau"]), trace_logZ=np.stack(trace["logZ"]),
+               trace_ess=np.stack(trace["ess"]), **draws)
+    save("smc_replay_m71_tiles.npz", **out)
+
+
+# ----------------------------------------------------------------------------
+def gen_stats(which, seeds):
+    """Statistical targets: reference SMCsampler.run() over many seeds."""
+    import contextlib
+    import io
+    torch.set_num_threads(8)
+    if which == "basic":
+        res = basic_truth_image(16, 1)
+        img = res[-1][0]
+        pr = basic_prior(16, 3, 3)
+        mk = lambda: SingleComponentMH(100, 0.1, 100, pr.flux_scale, 1e6)  # noqa: E731
+        model, tile, N, method = basic_model(16), 16, 256, "systematic"
+    elif which == "m71":
+        res = m71_truth_image(8, 0)
+        img = res[-1][0]
+        pr = m71_prior(8, 10, 10)
+        mk = lambda: SingleComponentMH(100, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])  # noqa
+        model, tile, N, method = m71_model(8), 8, 1000, "systematic"
+    else:
+        raise ValueError(which)
+    rows = []
+    for seed in seeds:
+        torch.manual_seed(seed)
+        s = sampler_for(img, tile, pr, model, mk(), N, method=method)
+        esses = []
+        orig_uw = s.update_weights
+
+        def uw(s=s, esses=esses, orig_uw=orig_uw):
+            orig_uw()
+            esses.append(float(s.ess.flatten()[0]))
+
+        s.update_weights = uw
+        t0 = time.perf_counter()
+        with contextlib.redirect_stdout(io.StringIO()):
+            s.run()
+        dt = time.perf_counter() - t0
+        pc = s.pruned_counts.flatten()
+        hist = np.bincount(pc.numpy().astype(np.int64), minlength=pr.max_objects + 1)
+        rows.append(dict(seed=seed, logZ=float(s.log_normalizing_constant.flatten()[0]),
+                         iters=int(s.iter), ess_trace=esses,
+                         final_ess=float(s.ess.flatten()[0]),
+                         pruned_hist=(hist / hist.sum()).tolist(),
+                         mean_total_flux=float(s.posterior_mean_total_flux(s.fluxes).flatten()[0]),
+                         mean_total_flux_pruned=float(
+                             s.posterior_mean_total_flux(s.pruned_fluxes).flatten()[0]),
+                         runtime_s=dt))
+        print(which, seed, rows[-1]["logZ"], rows[-1]["iters"], f"{dt:.1f}s", flush=True)
+    cfg = dict(which=which, tile=tile, N=N, S=pr.max_objects, K=100, method=method,
+               rho=0.5, torch_threads=torch.get_num_threads())
+    path = os.path.join(HERE, f"stats_{which}.json")
+    with open(path, "w") as f:
+        json.dump(dict(config=cfg, image=img.numpy().tolist(), runs=rows), f)
+    print("wrote", path)
+
+
+if __name__ == "__main__":
+    torch.set_default_dtype(torch.float32)
+    what = sys.argv[1] if len(sys.argv) > 1 else "fixtures"
+    if what == "fixtures":
+        gen_psf()
+        gen_loglik()
+        gen_prior()
+        gen_distributions()
+        gen_mh()
+        gen_smc_steps()
+        gen_smc_replay()
+    elif what == "stats":
+        which = sys.argv[2]
+        n = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+        gen_stats(which, list(range(n)))
+    else:
+        raise SystemExit(f"unknown target {what}")
