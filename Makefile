@@ -1,0 +1,26 @@
+# Builds the gfx950 HIP hot path (smcdet_amd/libsmcdet_hip.so) and the C oracle.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
+CSRC := smcdet_amd/csrc
+SRCS := $(CSRC)/common.hip $(CSRC)/model_kernels.hip $(CSRC)/mh_kernel.hip $(CSRC)/smc_kernels.hip
+HDRS := $(CSRC)/device.h $(CSRC)/render.h include/smcdet_hip.h
+OBJS := $(SRCS:.hip=.o)
+LIB := smcdet_amd/libsmcdet_hip.so
+
+all: $(LIB) oracle
+
+$(CSRC)/%.o: $(CSRC)/%.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -f $(OBJS) $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all clean oracle

@@ -1,0 +1,258 @@
+#!/usr/bin/env python
+"""Benchmark: MH particle-steps/sec on 4096-particle 32x32 synthetic M71 tiles.
+
+Workload (BASELINE.json configs[1]): one 32x32 tile per GPU,
+S = 10 sources per catalog, N = 4096 particles, SingleComponentMH with 100
+iterations per SMC step, M71 image model/prior (notebooks/smc.ipynb params,
+counts_rate 5/(40*40)), systematic resampling, rho = 0.5.
+
+A timed "step" is one full SMC iteration of the hot path on resident device
+data: the fused MH sweep (ancestor gather + 100 MH iterations + fresh
+log-likelihood) and the per-tile temper + reweight + resampling-index launch.
+particle-steps per step = N * 100 per tile.  Multi-GPU: one process per GPU,
+each rank owns its own tile(s) (weak scaling, no data-path collective); the
+timed region is bracketed by barrier + synchronize and the MAX over ranks is
+reported.  value = all ranks' particle-steps / that time.
+
+Roofline objects: `roofline` (HBM, as BASELINE.json asks): algorithmic bytes
+of the MH launch = 248 B per particle-step (state read+write
+24*S B + log-target cache 8 B) x N x K over the MH kernel's average
+duration, timed with HIP events on the launch stream.  `compute` gives the
+binding resource (FP32 VALU + transcendental) with SURVEY §8d's algorithmic
+68.0 kFLOP / 13.6 k transcendentals per particle-step of the reference's full
+re-render.  `cpu_baseline`: the C restatement (oracle/mh_oracle.c, float64,
+OpenMP) timed on this host's cores on a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+M71 = dict(flux_alpha=0.21411753249015655, flux_lower=0.06291294097900389,
+           flux_upper=1804.6791992187502, flux_detection_threshold=0.25165176391601557,
+           background=104.1486587524414, adu_per_nmgy=241.02658081054688,
+           psf_params=[1.107237458229065, 2.0800251960754395, 2.3254318237304688,
+                       5.240590572357178, 0.7346734404563904, 0.5114791393280029],
+           psf_radius=8, noise_additive=1.0000007072408224e-10,
+           noise_multiplicative=1.936462640762329)
+COUNTS_RATE_C2 = 5.0 / (40 * 40)
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md (spec)
+FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md (vector FP32, spec)
+B_ALG_PER_STEP = 248        # SURVEY §8d, S=10
+F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--particles", type=int, default=4096)
+    ap.add_argument("--tile", type=int, default=32)
+    ap.add_argument("--sources", type=int, default=10)
+    ap.add_argument("--mh-iters", type=int, default=100)
+    ap.add_argument("--tiles-per-gpu", type=int, default=1)
+    ap.add_argument("--full-recompute", action="store_true")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def make_models(H, S):
+    from smcdet_amd.images import M71ImageModel
+    from smcdet_amd.kernel import SingleComponentMH
+    from smcdet_amd.prior import M71Prior
+    p = M71
+    model = M71ImageModel(image_height=H, image_width=H, background=p["background"],
+                          psf_radius=p["psf_radius"], adu_per_nmgy=p["adu_per_nmgy"],
+                          psf_params=p["psf_params"], noise_additive=p["noise_additive"],
+                          noise_multiplicative=p["noise_multiplicative"])
+    prior = M71Prior(min_objects=S, max_objects=S, counts_rate=COUNTS_RATE_C2, image_height=H,
+                     image_width=H, flux_alpha=p["flux_alpha"], flux_lower=p["flux_lower"],
+                     flux_upper=p["flux_upper"], pad=4)
+    truth = M71Prior(min_objects=0, max_objects=100, counts_rate=COUNTS_RATE_C2, image_height=H,
+                     image_width=H, flux_alpha=p["flux_alpha"],
+                     flux_lower=p["flux_detection_threshold"], flux_upper=p["flux_upper"], pad=4)
+    return model, prior, truth, SingleComponentMH
+
+
+def synthetic_image(model, truth, H, tiles_per_side, seed, dev, max_sources):
+    """Synthetic M71 truth tiles (generate_images, images.py:178-228), drawn on
+    device; draws with more than max_sources sources are rejected."""
+    torch.manual_seed(seed)
+    img = torch.empty(tiles_per_side * H, tiles_per_side * H, device=dev)
+    for a in range(tiles_per_side):
+        for b in range(tiles_per_side):
+            while True:
+                c, l, f = truth.sample(num_catalogs=1, device=dev)
+                if int(c.max()) <= max_sources:
+                    break
+            img[a * H:(a + 1) * H, b * H:(b + 1) * H] = model.sample(l, f)[0, 0, :, :, 0]
+    return img
+
+
+def cpu_baseline(args, image_tile, seconds):
+    """C restatement of the reference MH sweep (float64 full re-render per
+    step, OpenMP over particles) on a bounded sample of the same workload."""
+    import numpy as np
+
+    from oracle import c_oracle
+    from oracle import smc_oracle as O
+    H, S = args.tile, args.sources
+    p = M71
+    model = O.M71Model(H, H, p["background"], p["psf_radius"], p["adu_per_nmgy"],
+                       p["psf_params"], p["noise_additive"], p["noise_multiplicative"])
+    prior = O.M71PriorP(S, S, COUNTS_RATE_C2, H, H, 4, p["flux_alpha"], p["flux_lower"],
+                        p["flux_upper"])
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    rng = np.random.default_rng(0)
+    n = max(64, 8 * threads)
+    locs = (rng.random((1, 1, n, S, 2)) * (H + 8) - 4).astype(np.float32)
+    fl = O.trunc_pareto_sample(rng.random((1, 1, n, S)), p["flux_alpha"], p["flux_lower"],
+                               p["flux_upper"]).astype(np.float32)
+    counts = np.full((1, 1, n), S, np.float32)
+    img = image_tile.reshape(1, 1, H, H)
+    c_oracle.lib()
+    # calibrate K so the timed sample takes ~`seconds`
+    K = 2
+    while True:
+        mh = O.MHParams(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"])
+        t0 = time.perf_counter()
+        c_oracle.mh_sweep(img, counts, locs, fl, 0.3, prior, model, mh, seed=1, threads=threads)
+        dt = time.perf_counter() - t0
+        if dt > seconds / 4 or K >= 4096:
+            break
+        K *= 2
+    K = max(1, int(K * seconds / max(dt, 1e-6)))
+    mh = O.MHParams(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"])
+    t0 = time.perf_counter()
+    c_oracle.mh_sweep(img, counts, locs, fl, 0.3, prior, model, mh, seed=2, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": n * K / dt, "unit": "particle-steps/sec", "cores": threads, "kind": "port",
+            "sample": f"oracle/mh_oracle.c float64 full re-render, {n} particles x {K} MH "
+                      f"iterations, {H}x{H} tile, S={S}, tau=0.3 ({dt:.1f} s)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if dist else 0)
+    torch.cuda.set_device(dev)
+
+    from smcdet_amd.sampler import SMCsampler
+    H, S, Np, K = args.tile, args.sources, args.particles, args.mh_iters
+    tps = int(round(args.tiles_per_gpu ** 0.5))
+    model, prior, truth, MH = make_models(H, S)
+    image = synthetic_image(model, truth, H, tps, 1000 + rank, dev, max_sources=S)
+    mh = MH(K, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"],
+            full_recompute=args.full_recompute)
+    s = SMCsampler(image, H, prior, model, mh, Np, 0.5, "systematic",
+                   M71["flux_detection_threshold"], 10 ** 9, print_every=10 ** 9,
+                   seed=12345 + rank, device=dev)
+    s.initialize()
+    s._temper_reweight(with_resample=True)
+
+    ev = []
+
+    def step(record):
+        idx, s._pending_idx = s._pending_idx, None
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        s.mutate(ancestors=idx)
+        if record:
+            e1.record()
+            ev.append((e0, e1))
+        s._temper_reweight(with_resample=True)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t)
+    mh_ms = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
+
+    T = tps * tps
+    steps_per_step = T * Np * K
+    value = world * steps_per_step * args.steps / elapsed
+    launch_steps = steps_per_step  # particle-steps per MH launch
+    achieved_gbs = B_ALG_PER_STEP * launch_steps / (mh_ms * 1e-3) / 1e9
+    mh_rate = launch_steps / (mh_ms * 1e-3)
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_mh_r01.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": "particle-steps/sec (4096 particles, 32x32 tile)",
+        "value": value,
+        "unit": "particle-steps/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (M71 prior + image model, seed 1000+rank)",
+        "config": {"workload": f"C2: {T} x {H}x{H} tile(s)/GPU, S={S}, N={Np}, "
+                               f"{K} MH iters per SMC step, systematic, rho=0.5",
+                   "tiles_per_gpu": T, "particles": Np, "tile": H, "sources": S,
+                   "mh_iters": K, "mode": "full" if args.full_recompute else "incremental",
+                   "parallelism": f"tile-sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "smcdet mh_sweep_kernel", "kernel_ms": mh_ms,
+                     "alg_bytes_per_particle_step": B_ALG_PER_STEP},
+        "compute": {"bound": "valu", "mh_particle_steps_per_s": mh_rate,
+                    "alg_flop_per_particle_step": F_ALG_PER_STEP,
+                    "achieved_alg_tflops": mh_rate * F_ALG_PER_STEP / 1e12,
+                    "peak_fp32_tflops": FP32_PEAK_TFLOPS,
+                    "frac": mh_rate * F_ALG_PER_STEP / 1e12 / FP32_PEAK_TFLOPS},
+        "smc": {"temperature_min": float(s.temperature.min()),
+                "acc_rate": float(s.mutation_acc_rates.mean()),
+                "ess_mean": float(s.ess.mean())},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args, image[:H, :H].cpu().numpy(),
+                                               args.cpu_baseline_seconds)
+        except Exception as e:  # report, never fail the bench line on it
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,205 @@
+/*
+ * smcdet_hip.h — C ABI of the MI355X (gfx950) hot path of the smcdet SMC
+ * star-detection sampler.  Plain pointers and sizes only; every buffer is a
+ * caller-owned, contiguous, float32 (unless stated) device allocation on the
+ * device that owns `stream`.  Every entry point is asynchronous on `stream`
+ * (a hipStream_t passed as void*), never allocates, never synchronises, and
+ * returns 0 on success or a negative SMCDET_E* code; smcdet_last_error()
+ * then describes the failure (thread-local).
+ *
+ * Layout follows the reference (timwhite0/smcdet): tiles lead, then
+ * particles, then sources.  T = numH*numW tiles (row-major), N particles per
+ * tile, S sources per particle (= Prior.max_objects), tile H x W pixels.
+ *   tiled_image [T,H,W]   locs [T,N,S,2] (row h, column w)   fluxes [T,N,S]
+ *   counts [T,N] (float32, as the reference)                  per-tile [T]
+ *
+ * Each entry point cites the reference interface it replaces.  The
+ * reference has no FFI: its "plugin" boundary is duck-typed Python objects
+ * (smcdet/sampler.py:10-37); the Python package smcdet_amd keeps those
+ * classes and calls this ABI through ctypes.
+ */
+#ifndef SMCDET_HIP_H
+#define SMCDET_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SMCDET_ABI_VERSION 1
+
+/* status codes */
+#define SMCDET_OK 0
+#define SMCDET_EINVAL -1      /* bad argument (null pointer, size, enum) */
+#define SMCDET_EUNSUPPORTED -2 /* shape outside what the kernels support */
+#define SMCDET_EHIP -3        /* HIP runtime error (launch/config) */
+
+/* image models */
+#define SMCDET_MODEL_M71 1     /* M71ImageModel: 3-component PSF, Gaussian noise */
+#define SMCDET_MODEL_POISSON 2 /* ImageModel: Normal-pdf PSF, Poisson noise      */
+
+/* priors */
+#define SMCDET_PRIOR_M71 1    /* M71Prior: Poisson count, uniform locs, truncated-Pareto flux */
+#define SMCDET_PRIOR_PARETO 2 /* ParetoStarPrior: uniform count, uniform locs, Pareto flux   */
+
+/* resampling */
+#define SMCDET_RESAMPLE_MULTINOMIAL 0
+#define SMCDET_RESAMPLE_SYSTEMATIC 1
+
+/* mh flags */
+#define SMCDET_MH_FULL_RECOMPUTE 1u /* re-render every source per step (reference arithmetic) */
+
+/* Image model (smcdet/images.py:6-26 ImageModel, :105-145 M71ImageModel). */
+typedef struct smcdet_image_model {
+  int32_t model;          /* SMCDET_MODEL_* */
+  int32_t H, W;           /* tile height / width in pixels */
+  int32_t psf_radius;     /* R: (2R+1)^2 window anchored at floor(loc) */
+  float background;       /* additive background (ADU) */
+  float adu_per_nmgy;     /* M71 flux scale; 1 for POISSON */
+  float psf_params[6];    /* M71: sigma1, sigma2, sigmap, beta, b, p0; POISSON: [0]=psf_stdev */
+  float psf_norm;         /* M71 normalising constant C (images.py:122-135) */
+  float noise_additive;   /* M71: variance = noise_additive + noise_multiplicative*rate */
+  float noise_multiplicative;
+} smcdet_image_model_t;
+
+/* Prior (smcdet/prior.py:8-75, :78-101, :157-189, :192-226). */
+typedef struct smcdet_prior {
+  int32_t kind;           /* SMCDET_PRIOR_* */
+  int32_t min_objects, max_objects;
+  float loc_low;          /* -pad */
+  float loc_high_h;       /* H + pad */
+  float loc_high_w;       /* W + pad */
+  float poisson_mean;     /* M71: counts_rate*(H+2pad)*(W+2pad) */
+  float flux_alpha;
+  float flux_lower;       /* M71: truncated-Pareto lower; PARETO: flux_scale */
+  float flux_upper;       /* M71: truncated-Pareto upper; PARETO: unused */
+} smcdet_prior_t;
+
+/* Single-component MH kernel (smcdet/kernel.py:7-24). */
+typedef struct smcdet_mh {
+  int32_t num_iters;
+  float locs_stdev;
+  float fluxes_stdev;
+  float fluxes_min, fluxes_max;
+  float locs_min_h, locs_min_w; /* = Prior.loc_prior.low  (sampler.py:36) */
+  float locs_max_h, locs_max_w; /* = Prior.loc_prior.high (sampler.py:37) */
+} smcdet_mh_t;
+
+/* Optional replay of recorded draws (tests): per MH iteration k, tile t,
+ * particle n: the chosen component, the two location uniforms and the flux
+ * uniform of the chosen component, and the accept uniform. */
+typedef struct smcdet_mh_replay {
+  const int32_t* comp; /* [K,T,N]   */
+  const float* uloc;   /* [K,T,N,2] */
+  const float* uflux;  /* [K,T,N]   */
+  const float* uacc;   /* [K,T,N]   */
+} smcdet_mh_replay_t;
+
+const char* smcdet_version(void);
+int32_t smcdet_abi_version(void);
+const char* smcdet_last_error(void);
+
+/* ImageModel.loglikelihood / M71ImageModel.loglikelihood
+ * (smcdet/images.py:85-102, :159-175): out[T,N]. */
+int smcdet_loglik(const smcdet_image_model_t* model, const float* tiled_image,
+                  const float* locs, const float* fluxes, int32_t T, int32_t N,
+                  int32_t S, float* out, void* stream);
+
+/* rate image lambda = B + sum_j g*f_j*psf_j  (images.py:80-82, :149-154):
+ * rate[T,H,W,N] (the layout the reference's ImageModel.sample produces). */
+int smcdet_render(const smcdet_image_model_t* model, const float* locs,
+                  const float* fluxes, int32_t T, int32_t N, int32_t S,
+                  float* rate, void* stream);
+
+/* ImageModel.psf (smcdet/images.py:28-76): dense psf[T,H,W,N,S]. */
+int smcdet_psf_dense(const smcdet_image_model_t* model, const float* locs,
+                     int32_t T, int32_t N, int32_t S, float* psf, void* stream);
+
+/* Noise draw for ImageModel.sample (images.py:78-83 Poisson, :147-157
+ * Normal): image[T,H,W,N] from rate[T,H,W,N] (in place allowed). */
+int smcdet_sample_image(const smcdet_image_model_t* model, const float* rate,
+                        int64_t count, uint64_t seed, uint64_t offset,
+                        float* image, void* stream);
+
+/* Prior.log_prob (smcdet/prior.py:67-75, :183-189, :220-226): out[T,N]. */
+int smcdet_log_prior(const smcdet_prior_t* prior, const float* counts,
+                     const float* locs, const float* fluxes, int32_t T,
+                     int32_t N, int32_t S, float* out, void* stream);
+
+/* Prior.sample(stratify_by_count=True, num_catalogs_per_count=n_per_count)
+ * (smcdet/prior.py:25-64, :201-217): N = (max-min+1)*n_per_count.
+ * uloc [T,N,S,2] / uflux [T,N,S] replay the uniforms when non-null. */
+int smcdet_prior_sample(const smcdet_prior_t* prior, int32_t T,
+                        int32_t n_per_count, uint64_t seed, uint64_t offset,
+                        const float* uloc, const float* uflux, float* counts,
+                        float* locs, float* fluxes, void* stream);
+
+/* SingleComponentMH.run (smcdet/kernel.py:26-130), K = mh->num_iters
+ * iterations fused in one launch.  Reads the state of particle
+ * ancestors[t,n] (identity when null) from *_in and writes the mutated
+ * state to *_out (in place allowed when ancestors is null).  counts_out may
+ * be null.  temperature[T].  Outputs: acc_rate[T] = acceptance rate of the
+ * LAST iteration (kernel.py:130); loglik_out[T,N] (nullable) = the image
+ * log-likelihood of the returned state (what SMCsampler.temper recomputes,
+ * sampler.py:100-102).  acc_count[T] is an int32 workspace. */
+int smcdet_mh_sweep(const smcdet_image_model_t* model,
+                    const smcdet_prior_t* prior, const smcdet_mh_t* mh,
+                    const float* tiled_image, const float* temperature,
+                    int32_t T, int32_t N, int32_t S, const int64_t* ancestors,
+                    const float* counts_in, const float* locs_in,
+                    const float* fluxes_in, float* counts_out,
+                    float* locs_out, float* fluxes_out, uint64_t seed,
+                    uint64_t offset, const smcdet_mh_replay_t* replay,
+                    uint32_t flags, float* loglik_out, float* acc_rate,
+                    int32_t* acc_count, void* stream);
+
+/* SMCsampler.temper (smcdet/sampler.py:93-125) on device: per tile, delta
+ * solves exp(2 LSE(delta*l) - LSE(2 delta*l)) = ess_threshold on (0, 1-tau]
+ * (or delta = 1-tau when the ESS there is still above threshold).
+ * temperature[T] is updated in place (float32 tau + delta); temperature_prev
+ * receives the old value. */
+int smcdet_temper(const float* loglik, float* temperature,
+                  float* temperature_prev, int32_t T, int32_t N,
+                  double ess_threshold, void* stream);
+
+/* SMCsampler.update_weights (smcdet/sampler.py:181-196). */
+int smcdet_update_weights(const float* loglik, const float* temperature,
+                          const float* temperature_prev,
+                          float* log_weights_unnorm, float* weights,
+                          float* ess, float* log_norm_const, int32_t T,
+                          int32_t N, void* stream);
+
+/* Resampling indices (smcdet/sampler.py:127-150): systematic
+ * (bucketize of (n+U)/N into cumsum(W)) or multinomial (iid).  u replays the
+ * uniforms when non-null ([T] systematic, [T,N] multinomial). */
+int smcdet_resample_index(const float* weights, int32_t T, int32_t N,
+                          int32_t method, uint64_t seed, uint64_t offset,
+                          const float* u, int64_t* idx, void* stream);
+
+/* temper + update_weights (+ resample index when idx != null) fused: one
+ * launch per SMC iteration instead of three. */
+int smcdet_temper_reweight(const float* loglik, float* temperature,
+                           float* temperature_prev, float* log_weights_unnorm,
+                           float* weights, float* ess, float* log_norm_const,
+                           int32_t T, int32_t N, double ess_threshold,
+                           int32_t resample_method, uint64_t seed,
+                           uint64_t offset, int64_t* idx, void* stream);
+
+/* Gather of the resampled state (smcdet/sampler.py:150-169). */
+int smcdet_gather(const int64_t* idx, int32_t T, int32_t N, int32_t S,
+                  const float* counts_in, const float* locs_in,
+                  const float* fluxes_in, float* counts_out, float* locs_out,
+                  float* fluxes_out, void* stream);
+
+/* SMCsampler.prune (smcdet/sampler.py:198-219): counts_out[T,N] int64,
+ * kept sources compacted to the front in their original order. */
+int smcdet_prune(const float* locs, const float* fluxes, int32_t T, int32_t N,
+                 int32_t S, float tile_dim, float flux_threshold,
+                 int64_t* counts_out, float* locs_out, float* fluxes_out,
+                 void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMCDET_HIP_H */

@@ -1,0 +1,98 @@
+"""ctypes wrapper of oracle/mh_oracle.c (CPU ORACLE / CPU BASELINE — test
+infrastructure only; never imported by the product package)."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from . import smc_oracle as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libmh_oracle.so")
+
+
+class _Model(ctypes.Structure):
+    _fields_ = [("model", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+                ("R", ctypes.c_int)] + [(k, ctypes.c_double) for k in (
+                    "bg", "g", "s1", "s2", "sp", "beta", "b", "p0", "norm", "psf_stdev",
+                    "s0sq", "eta")]
+
+
+class _Prior(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int), ("alpha", ctypes.c_double)]
+
+
+class _MH(ctypes.Structure):
+    _fields_ = [("K", ctypes.c_int)] + [(k, ctypes.c_double) for k in (
+        "sl", "sf", "lb_h", "lb_w", "ub_h", "ub_w", "lb_f", "ub_f")]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = ctypes.CDLL(LIB)
+        _lib.mh_oracle_sweep.restype = ctypes.c_int
+    return _lib
+
+
+def _pack(model, prior, mh):
+    m = _Model()
+    m.H, m.W, m.R = model.H, model.W, model.psf_radius
+    m.bg = model.background
+    if isinstance(model, O.M71Model):
+        m.model = 1
+        m.g = model.adu_per_nmgy
+        m.s1, m.s2, m.sp, m.beta, m.b, m.p0 = model.psf_params
+        m.norm = model.norm_const
+        m.s0sq, m.eta = model.noise_additive, model.noise_multiplicative
+    else:
+        m.model = 2
+        m.g = 1.0
+        m.psf_stdev = model.psf_stdev
+    p = _Prior()
+    p.kind = 1 if isinstance(prior, O.M71PriorP) else 2
+    p.alpha = float(np.float32(prior.flux_alpha))
+    h = _MH()
+    h.K = mh.num_iters
+    h.sl, h.sf = mh.locs_stdev, mh.fluxes_stdev
+    h.lb_h = h.lb_w = prior.loc_low
+    h.ub_h, h.ub_w = prior.loc_high
+    h.lb_f, h.ub_f = mh.fluxes_min, mh.fluxes_max
+    return m, p, h
+
+
+def mh_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mh, replay=None, seed=0,
+             threads=0):
+    """Runs the C sweep; returns (locs, fluxes, acc_rate[nH,nW])."""
+    img = np.ascontiguousarray(tiled_image, dtype=np.float32)
+    nH, nW, N, S, _ = np.shape(locs)
+    T = nH * nW
+    c = np.ascontiguousarray(counts, dtype=np.float32)
+    l = np.array(locs, dtype=np.float32, order="C")
+    f = np.array(fluxes, dtype=np.float32, order="C")
+    t = np.ascontiguousarray(np.broadcast_to(np.asarray(tau, np.float32), (nH, nW)))
+    acc = np.zeros((T, N), np.uint8)
+    m, p, h = _pack(model, prior, mh)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None else None  # noqa: E731
+    rc_ = ru = rf = ra = None
+    if replay is not None:
+        rc_ = np.ascontiguousarray(replay["comp"], dtype=np.int32)
+        ru = np.ascontiguousarray(replay["uloc"], dtype=np.float32)
+        rf = np.ascontiguousarray(replay["uflux"], dtype=np.float32)
+        ra = np.ascontiguousarray(replay["uacc"], dtype=np.float32)
+    lib().mh_oracle_sweep(ctypes.byref(m), ctypes.byref(p), ctypes.byref(h), P(img), P(c), P(l),
+                          P(f), P(t), T, N, S, P(rc_), P(ru), P(rf), P(ra),
+                          ctypes.c_uint64(seed), threads, P(acc))
+    return l, f, acc.reshape(nH, nW, N).mean(-1)

@@ -1,0 +1,129 @@
+"""ctypes binding of the gfx950 C ABI (include/smcdet_hip.h).
+
+The library `libsmcdet_hip.so` is built in-tree by `make` (or
+`__graft_entry__.build()`).  There is no fallback: if the library is missing
+or the tensors are not float32 CUDA(HIP) tensors, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SMCDET_HIP_LIB", os.path.join(_HERE, "libsmcdet_hip.so"))
+
+SMCDET_MODEL_M71 = 1
+SMCDET_MODEL_POISSON = 2
+SMCDET_PRIOR_M71 = 1
+SMCDET_PRIOR_PARETO = 2
+SMCDET_RESAMPLE_MULTINOMIAL = 0
+SMCDET_RESAMPLE_SYSTEMATIC = 1
+SMCDET_MH_FULL_RECOMPUTE = 1
+
+c_f = ctypes.c_float
+c_i = ctypes.c_int32
+c_p = ctypes.c_void_p
+c_u64 = ctypes.c_uint64
+c_i64 = ctypes.c_int64
+c_u32 = ctypes.c_uint32
+c_d = ctypes.c_double
+
+
+class ImageModelC(ctypes.Structure):
+    _fields_ = [("model", c_i), ("H", c_i), ("W", c_i), ("psf_radius", c_i),
+                ("background", c_f), ("adu_per_nmgy", c_f), ("psf_params", c_f * 6),
+                ("psf_norm", c_f), ("noise_additive", c_f), ("noise_multiplicative", c_f)]
+
+
+class PriorC(ctypes.Structure):
+    _fields_ = [("kind", c_i), ("min_objects", c_i), ("max_objects", c_i), ("loc_low", c_f),
+                ("loc_high_h", c_f), ("loc_high_w", c_f), ("poisson_mean", c_f),
+                ("flux_alpha", c_f), ("flux_lower", c_f), ("flux_upper", c_f)]
+
+
+class MHC(ctypes.Structure):
+    _fields_ = [("num_iters", c_i), ("locs_stdev", c_f), ("fluxes_stdev", c_f),
+                ("fluxes_min", c_f), ("fluxes_max", c_f), ("locs_min_h", c_f),
+                ("locs_min_w", c_f), ("locs_max_h", c_f), ("locs_max_w", c_f)]
+
+
+class ReplayC(ctypes.Structure):
+    _fields_ = [("comp", c_p), ("uloc", c_p), ("uflux", c_p), ("uacc", c_p)]
+
+
+_SIGS = {
+    "smcdet_version": ([], ctypes.c_char_p),
+    "smcdet_abi_version": ([], c_i),
+    "smcdet_last_error": ([], ctypes.c_char_p),
+    "smcdet_loglik": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
+    "smcdet_render": ([c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
+    "smcdet_psf_dense": ([c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
+    "smcdet_sample_image": ([c_p, c_p, c_i64, c_u64, c_u64, c_p, c_p], c_i),
+    "smcdet_log_prior": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
+    "smcdet_prior_sample": ([c_p, c_i, c_i, c_u64, c_u64, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
+    "smcdet_mh_sweep": ([c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p,
+                         c_p, c_u64, c_u64, c_p, c_u32, c_p, c_p, c_p, c_p], c_i),
+    "smcdet_temper": ([c_p, c_p, c_p, c_i, c_i, c_d, c_p], c_i),
+    "smcdet_update_weights": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p], c_i),
+    "smcdet_resample_index": ([c_p, c_i, c_i, c_i, c_u64, c_u64, c_p, c_p, c_p], c_i),
+    "smcdet_temper_reweight": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_d, c_i, c_u64,
+                                c_u64, c_p, c_p], c_i),
+    "smcdet_gather": ([c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
+    "smcdet_prune": ([c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p, c_p, c_p, c_p], c_i),
+}
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+
+
+def lib():
+    """Load libsmcdet_hip.so once (raises if it is missing: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"smcdet_amd: HIP library not found at {LIB_PATH}; build it with `make` "
+                "(or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def version() -> str:
+    return lib().smcdet_version().decode()
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().smcdet_last_error().decode()
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def dev_f32(t, name):
+    """Validates a float32 contiguous HIP tensor (no silent host fallback)."""
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must live on a HIP device (got {t.device}); "
+                           "smcdet_amd runs only on MI355X (gfx950)")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32 (got {t.dtype})")
+    return t.contiguous()
+
+
+def ref(x):
+    return ctypes.byref(x)

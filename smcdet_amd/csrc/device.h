@@ -1,0 +1,192 @@
+// device.h — shared device-side helpers for the smcdet MI355X (gfx950) kernels:
+// Philox4x32-10 counter-based RNG, 64-lane wave reductions, the two PSF
+// profiles and the two per-pixel log-likelihoods of the reference's image
+// models (timwhite0/smcdet smcdet/images.py).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/smcdet_hip.h"
+
+namespace smcdet {
+
+constexpr int kWave = 64;
+constexpr float kHalfLog2Pi = 0.91893853320467274178f;  // 0.5*log(2*pi)
+constexpr float kLn2 = 0.69314718055994530942f;
+constexpr float kLog2e = 1.44269504088896340736f;
+constexpr float kSqrt2 = 1.41421356237309504880f;
+constexpr float kSqrt1_2 = 0.70710678118654752440f;
+
+// ---------------------------------------------------------------------------
+// host-side error reporting (defined in common.hip)
+// ---------------------------------------------------------------------------
+int set_error(int code, const char* fmt, ...);
+int check_launch(const char* what);
+// raises the kernel's dynamic-LDS limit when bytes > 64 KiB (<= 160 KiB)
+int ensure_lds(const void* kernel, size_t bytes);
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al. 2011) — counter (c0..c3), key (k0,k1)
+// ---------------------------------------------------------------------------
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox4x32(uint32_t c0, uint32_t c1, uint32_t c2,
+                                          uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c0;
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2);
+    c0 = hi1 ^ c1 ^ k0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ k1;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return U4{c0, c1, c2, c3};
+}
+
+// [0,1) with 24 random mantissa bits, like torch.rand for float32
+__device__ __forceinline__ float u01(uint32_t x) {
+  return (float)(x >> 8) * 5.9604644775390625e-08f;
+}
+
+// stream tags keep the counter spaces of different draws disjoint
+enum RngTag : uint32_t {
+  kTagMH0 = 0x4d480000u,
+  kTagMH1 = 0x4d480001u,
+  kTagPriorLoc = 0x50520000u,
+  kTagPriorFlux = 0x50520001u,
+  kTagResample = 0x52530000u,
+  kTagNoise = 0x4e530000u,
+};
+
+// ---------------------------------------------------------------------------
+// wave helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float readlane(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ int readlane(int v, int lane) {
+  return __builtin_amdgcn_readlane(v, lane);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_logf(x); }
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// torch.nan_to_num(x) defaults: nan -> 0, +inf -> FLT_MAX, -inf -> -FLT_MAX
+__device__ __forceinline__ float nan_to_num(float x, float nan_val) {
+  if (x != x) return nan_val;
+  if (isinf(x)) return x > 0.f ? 3.402823466e+38f : -3.402823466e+38f;
+  return x;
+}
+
+// ---------------------------------------------------------------------------
+// image model, pre-digested for the device
+// ---------------------------------------------------------------------------
+struct DevModel {
+  int model, H, W, R;
+  float bg;     // background
+  float g;      // flux -> ADU scale (adu_per_nmgy; 1 for Poisson)
+  // M71: psf(r2) = (exp2(k1 r2) + b exp2(k2 r2) + p0 exp2(kb log2(1 + k3 r2))) * inv_norm
+  float k1, k2, b, k3, kb, p0, inv_norm;
+  // Poisson (basic) model: psf(r2) = amp * exp2(kg r2)
+  float kg, amp;
+  // M71 noise: var = s0sq + eta * rate
+  float s0sq, eta;
+};
+
+DevModel make_dev_model(const smcdet_image_model_t& m);  // common.hip
+int validate_model(const smcdet_image_model_t* m);        // common.hip
+
+// M71ImageModel._compute_normalized_psf (images.py:137-145) / the basic
+// model's Normal(0, sigma).log_prob(r).exp() (images.py:17, 25-26)
+template <int MODEL>
+__device__ __forceinline__ float psf_eval(const DevModel& m, float r2) {
+  if constexpr (MODEL == SMCDET_MODEL_M71) {
+    const float t1 = fast_exp2(m.k1 * r2);
+    const float t2 = fast_exp2(m.k2 * r2);
+    const float t3 = fast_exp2(m.kb * fast_log2(fmaf(m.k3, r2, 1.0f)));
+    return (t1 + fmaf(m.b, t2, m.p0 * t3)) * m.inv_norm;
+  } else {
+    return m.amp * fast_exp2(m.kg * r2);
+  }
+}
+
+// per-pixel log-likelihood: M71 Normal(rate, sqrt(s0^2 + eta*rate)).log_prob(x)
+// (images.py:169-175); basic Poisson(rate).log_prob(x), Normal(rate, sqrt(rate))
+// where rate > 5e4 (images.py:91-102).  lgx = lgamma(x + 1).
+template <int MODEL>
+__device__ __forceinline__ float pix_loglik(const DevModel& m, float x, float lgx, float rate) {
+  const float d = x - rate;
+  if constexpr (MODEL == SMCDET_MODEL_M71) {
+    const float v = fmaf(m.eta, rate, m.s0sq);
+    return fmaf(-0.5f * d * d, fast_rcp(v), -0.5f * kLn2 * fast_log2(v) - kHalfLog2Pi);
+  } else {
+    const float lr = kLn2 * fast_log2(rate);
+    if (rate > 50000.0f) return fmaf(-0.5f * d * d, fast_rcp(rate), -0.5f * lr - kHalfLog2Pi);
+    return fmaf(x, lr, -rate) - lgx;
+  }
+}
+
+// Normal(mu, sigma).cdf(v) as torch computes it
+__device__ __forceinline__ float normal_cdf(float v, float mu, float inv_sigma) {
+  return 0.5f * (1.0f + erff((v - mu) * inv_sigma * kSqrt1_2));
+}
+
+struct DevPrior {
+  int kind;
+  float lo, hi_h, hi_w;
+  float count_c0, count_c1;  // M71: log(mu), mu ; PARETO: log(1/k), unused
+  int min_objects, max_objects;
+  float flux_c;              // log-normaliser of the flux density
+  float ap1;                 // alpha + 1
+  float alpha, lower, upper;
+  float loc_lp_h, loc_lp_w;  // -log(high - low) per coordinate
+};
+
+DevPrior make_dev_prior(const smcdet_prior_t& p);  // common.hip
+int validate_prior(const smcdet_prior_t* p);        // common.hip
+
+// ---------------------------------------------------------------------------
+// LDS image staging: x and (Poisson) lgamma(x+1) for one tile
+// ---------------------------------------------------------------------------
+template <int MODEL>
+__device__ __forceinline__ void stage_image(const float* __restrict__ img, float* xs, float* lg,
+                                            int HW, int tid, int nthreads) {
+  for (int p = tid; p < HW; p += nthreads) {
+    const float x = img[p];
+    xs[p] = x;
+    if constexpr (MODEL == SMCDET_MODEL_POISSON) lg[p] = lgammaf(x + 1.0f);
+  }
+}
+
+}  // namespace smcdet

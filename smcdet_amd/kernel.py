@@ -1,0 +1,120 @@
+"""Mutation kernel (drop-in for smcdet/kernel.py:7-130, SingleComponentMH).
+
+`SingleComponentMH.run(data, counts, locs, fluxes, temperature, log_target)`
+keeps the reference signature and return value `[locs, fluxes, acc_rate]`.
+The reference evaluates `log_target` (a Python callback, sampler.py:87-91) in
+every iteration; a fused gfx950 kernel cannot call back into Python, so the
+callback is resolved once to the (Prior, ImageModel) pair it closes over —
+the bound `SMCsampler.log_target`, or the `prior=`/`image_model=` keywords —
+and all `num_iters` iterations run in one launch
+(smcdet_amd/csrc/mh_kernel.hip).  Priors/image models without a HIP
+description raise NotImplementedError: there is no fallback dispatch.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _hip
+from ._rng import PhiloxStream
+
+
+def _f32(x):
+    return float(np.float32(float(x)))
+
+
+class SingleComponentMH(object):
+    def __init__(self, num_iters, locs_stdev, fluxes_stdev, fluxes_min, fluxes_max, *,
+                 full_recompute=False):
+        self.num_iters = num_iters
+        self.locs_stdev = torch.tensor(locs_stdev)
+        self.locs_min = None  # defined automatically within SMCsampler
+        self.locs_max = None  # defined automatically within SMCsampler
+        self.fluxes_stdev = fluxes_stdev * torch.ones(1)
+        self.fluxes_min = fluxes_min * torch.ones(1)
+        self.fluxes_max = fluxes_max * torch.ones(1)
+        # True: re-render every source at every step (the reference's arithmetic);
+        # False: incremental delta log-likelihood over the moved source's windows
+        self.full_recompute = full_recompute
+        self.rng = None           # PhiloxStream; SMCsampler installs its own
+        self.last_loglik = None   # log-likelihood of the state returned by run()
+
+    @staticmethod
+    def _resolve(log_target, prior, image_model):
+        if prior is None or image_model is None:
+            owner = getattr(log_target, "__self__", None)
+            if owner is None or not hasattr(owner, "Prior") or not hasattr(owner, "ImageModel"):
+                raise NotImplementedError(
+                    "SingleComponentMH.run needs log_target bound to an SMCsampler (or the "
+                    "prior=/image_model= keywords): arbitrary Python targets cannot run inside "
+                    "the fused HIP kernel")
+            prior = prior or owner.Prior
+            image_model = image_model or owner.ImageModel
+        return prior, image_model
+
+    def _cmh(self, prior):
+        c = _hip.MHC()
+        c.num_iters = int(self.num_iters)
+        c.locs_stdev = _f32(self.locs_stdev)
+        c.fluxes_stdev = _f32(self.fluxes_stdev.reshape(-1)[0])
+        c.fluxes_min = _f32(self.fluxes_min.reshape(-1)[0])
+        c.fluxes_max = _f32(self.fluxes_max.reshape(-1)[0])
+        lo = self.locs_min if self.locs_min is not None else prior.loc_prior.low
+        hi = self.locs_max if self.locs_max is not None else prior.loc_prior.high
+        lo = torch.as_tensor(lo).reshape(-1).cpu().float()
+        hi = torch.as_tensor(hi).reshape(-1).cpu().float()
+        c.locs_min_h, c.locs_min_w = float(lo[0]), float(lo[-1])
+        c.locs_max_h, c.locs_max_w = float(hi[0]), float(hi[-1])
+        return c
+
+    def run(self, data, counts, locs, fluxes, temperature, log_target=None, *, prior=None,
+            image_model=None, ancestors=None, replay=None, want_loglik=True):
+        """kernel.py:26-130.  ancestors [numH,numW,N] (int64, optional) gathers
+        the starting state (a fused resample); replay = dict(comp, uloc, uflux,
+        uacc) replays recorded draws."""
+        prior, image_model = self._resolve(log_target, prior, image_model)
+        data = _hip.dev_f32(data, "data")
+        counts = _hip.dev_f32(counts, "counts")
+        locs = _hip.dev_f32(locs, "locs")
+        fluxes = _hip.dev_f32(fluxes, "fluxes")
+        dev = locs.device
+        temperature = _hip.dev_f32(torch.as_tensor(temperature, device=dev, dtype=torch.float32),
+                                   "temperature")
+        nH, nW, N, S, _ = locs.shape
+        T = nH * nW
+        if temperature.numel() != T:
+            raise ValueError(f"temperature has {temperature.numel()} entries, need {T}")
+        if self.rng is None:
+            self.rng = PhiloxStream()
+        locs_out = torch.empty_like(locs)
+        fluxes_out = torch.empty_like(fluxes)
+        counts_out = None
+        anc_p = None
+        if ancestors is not None:
+            ancestors = ancestors.to(device=dev, dtype=torch.int64).contiguous()
+            counts_out = torch.empty_like(counts)
+            anc_p = _hip.ptr(ancestors)
+        acc = torch.empty(nH, nW, device=dev, dtype=torch.float32)
+        acc_ws = torch.empty(T, device=dev, dtype=torch.int32)
+        ll = torch.empty(nH, nW, N, device=dev, dtype=torch.float32) if want_loglik else None
+        rp = None
+        keep = []
+        if replay is not None:
+            rc = replay["comp"].to(device=dev, dtype=torch.int32).contiguous()
+            ru = [_hip.dev_f32(replay[k].to(dev), k) for k in ("uloc", "uflux", "uacc")]
+            keep = [rc] + ru
+            rp = _hip.ReplayC(_hip.ptr(rc).value, _hip.ptr(ru[0]).value, _hip.ptr(ru[1]).value,
+                              _hip.ptr(ru[2]).value)
+        off = self.rng.take(self.num_iters)
+        cm, cp, ch = image_model._cmodel(), prior._cprior(), self._cmh(prior)
+        flags = _hip.SMCDET_MH_FULL_RECOMPUTE if self.full_recompute else 0
+        _hip.check(_hip.lib().smcdet_mh_sweep(
+            _hip.ref(cm), _hip.ref(cp), _hip.ref(ch), _hip.ptr(data), _hip.ptr(temperature),
+            T, N, S, anc_p, _hip.ptr(counts), _hip.ptr(locs), _hip.ptr(fluxes),
+            _hip.ptr(counts_out), _hip.ptr(locs_out), _hip.ptr(fluxes_out), self.rng.seed, off,
+            _hip.ref(rp) if rp is not None else None, flags, _hip.ptr(ll), _hip.ptr(acc),
+            _hip.ptr(acc_ws), _hip.stream_of(locs)), "smcdet_mh_sweep")
+        del keep
+        self.last_loglik = ll
+        self.last_counts = counts_out if counts_out is not None else counts
+        return [locs_out, fluxes_out, acc]

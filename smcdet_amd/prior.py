@@ -1,0 +1,219 @@
+"""Marked point-process priors (drop-in for smcdet/prior.py).
+
+Kept: `PointProcessPrior` (prior.py:8-75), `PoissonProcessPrior` (:78-101),
+`ParetoStarPrior` (:157-189), `M71Prior` (:192-226) with the reference
+constructors, attributes, `sample()` and `log_prob()`.
+
+`sample(stratify_by_count=True, ...)` — what SMCsampler.initialize uses — and
+`log_prob` run as gfx950 kernels (smcdet_prior_sample / smcdet_log_prior).
+The non-stratified `sample()` draw (used only to generate synthetic truth
+catalogs, images.py:186) is plain torch on the HIP device.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+from torch.distributions import Uniform
+
+from . import _hip
+from ._rng import PhiloxStream
+from .distributions import DiscreteUniform, TruncatedPareto
+
+
+def _f32(x):
+    return float(np.float32(x))
+
+
+def _device(device=None):
+    if device is not None:
+        return torch.device(device)
+    d = torch.get_default_device()
+    if d.type == "cuda":
+        return d
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class PointProcessPrior(object):
+    """prior.py:8-75: discrete-uniform count, uniform locations over the
+    padded tile [-pad, H+pad) x [-pad, W+pad)."""
+
+    def __init__(self, min_objects, max_objects, image_height, image_width, pad=0):
+        self.min_objects = min_objects
+        self.max_objects = max_objects
+        self.image_height = image_height
+        self.image_width = image_width
+        self.pad = pad
+        self.update_attrs()
+
+    def update_attrs(self):
+        self.num_counts = self.max_objects - self.min_objects + 1
+        self.count_prior = DiscreteUniform(self.min_objects, self.max_objects)
+        self.loc_prior = Uniform(
+            (0 - self.pad) * torch.ones(2, device="cpu"),
+            torch.tensor((self.image_height + self.pad, self.image_width + self.pad),
+                         dtype=torch.float32, device="cpu"))
+
+    # --- C-ABI description ----------------------------------------------------
+    def _cprior(self):
+        raise NotImplementedError(
+            f"{type(self).__name__} has no flux prior; the HIP path supports M71Prior and "
+            "ParetoStarPrior")
+
+    def _fill_common(self, c):
+        c.min_objects = int(self.min_objects)
+        c.max_objects = int(self.max_objects)
+        c.loc_low = _f32(-self.pad)
+        c.loc_high_h = _f32(self.image_height + self.pad)
+        c.loc_high_w = _f32(self.image_width + self.pad)
+        return c
+
+    def _sample_counts(self, shape, device):
+        idx = self.count_prior.sample(shape).long().cpu()
+        counts = torch.arange(self.min_objects, self.max_objects + 1)[idx]
+        return counts.to(device=device, dtype=torch.float32)
+
+    def _sample_flux(self, shape, device):
+        raise NotImplementedError
+
+    def sample(self, num_catalogs=1, num_tiles_per_side=1, stratify_by_count=False,
+               num_catalogs_per_count=None, device=None):
+        """prior.py:25-64 (+ the flux draws of :175-180, :212-217)."""
+        if stratify_by_count is True and num_catalogs_per_count is None:
+            raise ValueError("If stratify_by_count is True, need to specify catalogs_per_count.")
+        elif stratify_by_count is False and num_catalogs_per_count is not None:
+            raise ValueError("If stratify_by_count is False, do not specify catalogs_per_count.")
+        device = _device(device)
+        T = num_tiles_per_side
+        S = self.max_objects
+        if stratify_by_count:
+            self.num = self.num_counts * num_catalogs_per_count
+            counts, locs, fluxes = self.sample_stratified(T, num_catalogs_per_count,
+                                                          device=device)
+        else:
+            self.num = num_catalogs
+            counts = self._sample_counts([T, T, self.num], device)
+            lo, hi = self.loc_prior.low.to(device), self.loc_prior.high.to(device)
+            u = torch.rand(T, T, self.num, S, 2, device=device)
+            locs = lo + u * (hi - lo)
+            fluxes = self._sample_flux([T, T, self.num, S], device)
+            mask = torch.arange(S, device=device) < counts.unsqueeze(-1)
+            locs = locs * mask.unsqueeze(-1)
+            fluxes = fluxes * mask
+        self.counts_mask = torch.arange(S, device=device) < counts.unsqueeze(-1)
+        return [counts, locs, fluxes]
+
+    def sample_stratified(self, num_tiles_per_side, num_catalogs_per_count, device=None,
+                          rng: PhiloxStream | None = None, uloc=None, uflux=None):
+        """Stratified draw on device: counts = min..max (each repeated
+        num_catalogs_per_count times), uniform locs, prior fluxes, masked past
+        each count.  uloc/uflux replay the reference's torch.rand draws."""
+        device = _device(device)
+        T = num_tiles_per_side
+        N = self.num_counts * num_catalogs_per_count
+        S = self.max_objects
+        counts = torch.empty(T, T, N, device=device, dtype=torch.float32)
+        locs = torch.zeros(T, T, N, S, 2, device=device, dtype=torch.float32)
+        fluxes = torch.zeros(T, T, N, S, device=device, dtype=torch.float32)
+        rng = rng or PhiloxStream()
+        off = rng.take(T * T * N * S)
+        cp = self._cprior()
+        if uloc is not None:
+            uloc = _hip.dev_f32(uloc.to(device), "uloc")
+            uflux = _hip.dev_f32(uflux.to(device), "uflux")
+        _hip.check(_hip.lib().smcdet_prior_sample(
+            _hip.ref(cp), T * T, num_catalogs_per_count, rng.seed, off, _hip.ptr(uloc),
+            _hip.ptr(uflux), _hip.ptr(counts), _hip.ptr(locs), _hip.ptr(fluxes),
+            _hip.stream_of(counts)), "smcdet_prior_sample")
+        return counts, locs, fluxes
+
+    def log_prob(self, counts, locs, fluxes):
+        """prior.py:67-75 (+ flux terms of :183-189 / :220-226): [numH,numW,N]."""
+        counts = _hip.dev_f32(counts, "counts")
+        locs = _hip.dev_f32(locs, "locs")
+        fluxes = _hip.dev_f32(fluxes, "fluxes")
+        nH, nW, n, d, _ = locs.shape
+        out = torch.empty(nH, nW, n, device=locs.device, dtype=torch.float32)
+        cp = self._cprior()
+        _hip.check(_hip.lib().smcdet_log_prior(_hip.ref(cp), _hip.ptr(counts), _hip.ptr(locs),
+                                               _hip.ptr(fluxes), nH * nW, n, d, _hip.ptr(out),
+                                               _hip.stream_of(locs)), "smcdet_log_prior")
+        self.counts_mask = torch.arange(d, device=counts.device) < counts.unsqueeze(-1)
+        return out
+
+
+class PoissonProcessPrior(PointProcessPrior):
+    """prior.py:78-101: Poisson(counts_rate * (H+2pad)(W+2pad)) count prior."""
+
+    def __init__(self, min_objects, max_objects, counts_rate, image_height, image_width, pad=0):
+        self.min_objects = min_objects
+        self.max_objects = max_objects
+        self.counts_rate = counts_rate
+        self.image_height = image_height
+        self.image_width = image_width
+        self.pad = pad
+        self.update_attrs()
+
+    def update_attrs(self):
+        self.num_counts = self.max_objects - self.min_objects + 1
+        self.count_prior = torch.distributions.Poisson(
+            torch.tensor(self.poisson_mean, dtype=torch.float32))
+        self.loc_prior = Uniform(
+            (0 - self.pad) * torch.ones(2, device="cpu"),
+            torch.tensor((self.image_height + self.pad, self.image_width + self.pad),
+                         dtype=torch.float32, device="cpu"))
+
+    @property
+    def poisson_mean(self):
+        return _f32(self.counts_rate * (self.image_height + 2 * self.pad)
+                    * (self.image_width + 2 * self.pad))
+
+
+class ParetoStarPrior(PointProcessPrior):
+    """prior.py:157-189: Pareto(flux_scale, flux_alpha) fluxes."""
+
+    def __init__(self, *args, flux_scale, flux_alpha, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.flux_scale = flux_scale
+        self.flux_alpha = flux_alpha
+        self.flux_prior = torch.distributions.Pareto(torch.tensor(float(flux_scale)),
+                                                     torch.tensor(float(flux_alpha)))
+
+    def _sample_flux(self, shape, device):
+        u = torch.rand(*shape, device=device)
+        return _f32(self.flux_scale) * (1.0 - u) ** (-1.0 / _f32(self.flux_alpha))
+
+    def _cprior(self):
+        c = self._fill_common(_hip.PriorC())
+        c.kind = _hip.SMCDET_PRIOR_PARETO
+        c.flux_alpha = _f32(self.flux_alpha)
+        c.flux_lower = _f32(self.flux_scale)
+        c.flux_upper = 0.0
+        return c
+
+
+class M71Prior(PoissonProcessPrior):
+    """prior.py:192-226: Poisson counts, truncated-Pareto(alpha, lower, upper) fluxes."""
+
+    def __init__(self, *args, flux_alpha, flux_lower, flux_upper, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.flux_alpha = flux_alpha
+        self.flux_lower = flux_lower
+        self.flux_upper = flux_upper
+        self.flux_prior = TruncatedPareto(flux_alpha, flux_lower, flux_upper)
+
+    def _sample_flux(self, shape, device):
+        return self.flux_prior.sample(shape, device=device)
+
+    def _sample_counts(self, shape, device):
+        k = torch.poisson(torch.full(shape, self.poisson_mean, dtype=torch.float32)).long()
+        counts = torch.arange(self.min_objects, self.max_objects + 1)[k]
+        return counts.to(device=device, dtype=torch.float32)
+
+    def _cprior(self):
+        c = self._fill_common(_hip.PriorC())
+        c.kind = _hip.SMCDET_PRIOR_M71
+        c.poisson_mean = self.poisson_mean
+        c.flux_alpha = _f32(self.flux_alpha)
+        c.flux_lower = _f32(self.flux_lower)
+        c.flux_upper = _f32(self.flux_upper)
+        return c

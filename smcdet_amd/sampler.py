@@ -1,0 +1,312 @@
+"""Likelihood-tempered SMC sampler (drop-in for smcdet/sampler.py:9-298).
+
+`SMCsampler` keeps the reference constructor, methods (`initialize`,
+`log_target`, `tempering_objective`, `temper`, `resample`, `mutate`,
+`update_weights`, `prune`, `run`, `summarize`, posterior summaries) and the
+public attributes drivers read after `run()`.  Every per-particle step runs as
+a gfx950 kernel on the HIP device:
+
+    initialize   -> smcdet_prior_sample + smcdet_loglik
+    temper       -> smcdet_temper      (device root-find; the reference copies
+                                        the log-likelihoods to the host for
+                                        scipy brentq, sampler.py:99-125)
+    update_weights -> smcdet_update_weights
+    resample     -> smcdet_resample_index + smcdet_gather
+    mutate       -> smcdet_mh_sweep    (all num_iters MH iterations, one launch)
+    prune        -> smcdet_prune
+
+`run()` uses the fused schedule: per SMC iteration one MH launch (which also
+gathers the resampled ancestors and returns the log-likelihood of the new
+state) and one per-tile launch doing temper + reweight + the next resampling
+indices, with one 4-byte-per-tile device->host read for the loop condition.
+The random-stream order is the same as calling the methods one by one.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _hip
+from ._rng import PhiloxStream
+
+
+class SMCsampler(object):
+    def __init__(self, image, tile_dim, Prior, ImageModel, MutationKernel, num_catalogs,
+                 ess_threshold_prop, resample_method, flux_detection_threshold, max_smc_iters,
+                 print_every=5, *, seed=None, device=None, fused=True):
+        if device is None:
+            device = image.device if image.is_cuda else torch.device(
+                "cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        self.image = image.to(self.device, torch.float32)
+        self.image_dim = image.shape[0]
+
+        self.tile_dim = tile_dim
+        self.num_tiles_per_side = self.image_dim // self.tile_dim
+        self.tiled_image = (self.image.unfold(0, self.tile_dim, self.tile_dim)
+                            .unfold(1, self.tile_dim, self.tile_dim).contiguous())
+
+        self.Prior = Prior
+        self.ImageModel = ImageModel
+        self.MutationKernel = MutationKernel
+        self.MutationKernel.locs_min = self.Prior.loc_prior.low
+        self.MutationKernel.locs_max = self.Prior.loc_prior.high
+
+        self.num_catalogs = num_catalogs
+        self.ess_threshold = ess_threshold_prop * num_catalogs
+
+        if resample_method not in {"multinomial", "systematic"}:
+            raise ValueError("resample_method must be either multinomial or systematic.")
+        self.resample_method = resample_method
+        self.flux_detection_threshold = flux_detection_threshold
+        self.max_smc_iters = max_smc_iters
+        self.print_every = print_every
+        self.has_run = False
+
+        self.rng = PhiloxStream(seed)
+        self.MutationKernel.rng = self.rng
+        self.fused = fused
+        self._fresh_loglik = None   # loglik of the current state, if already known
+        self._pending_idx = None    # resampling indices computed by the fused tile launch
+
+    # ------------------------------------------------------------------ helpers
+    @property
+    def _T(self):
+        return self.num_tiles_per_side * self.num_tiles_per_side
+
+    def _zeros_tiles(self):
+        nt = self.num_tiles_per_side
+        return torch.zeros(nt, nt, device=self.device, dtype=torch.float32)
+
+    def _method_code(self):
+        return (_hip.SMCDET_RESAMPLE_SYSTEMATIC if self.resample_method == "systematic"
+                else _hip.SMCDET_RESAMPLE_MULTINOMIAL)
+
+    def _resample_offset(self, N):
+        return self.rng.take(1 if self.resample_method == "systematic" else N)
+
+    # ------------------------------------------------------------ the methods
+    def initialize(self):
+        """sampler.py:57-85."""
+        nt = self.num_tiles_per_side
+        self.counts, self.locs, self.fluxes = self.Prior.sample_stratified(
+            nt, self.num_catalogs, device=self.device, rng=self.rng)
+        self.Prior.num = self.counts.shape[-1]
+        self.temperature_prev = self._zeros_tiles()
+        self.temperature = self._zeros_tiles()
+        self.loglik = self.ImageModel.loglikelihood(self.tiled_image, self.locs, self.fluxes)
+        self._fresh_loglik = self.loglik
+        N = self.counts.shape[-1]
+        self.weights_log_unnorm = torch.zeros(nt, nt, N, device=self.device)
+        self.weights = torch.full((nt, nt, N), 1.0 / N, device=self.device)
+        self.log_normalizing_constant = self._zeros_tiles()
+        self.ess = torch.full((nt, nt), float(N), device=self.device)
+        self._pending_idx = None
+
+    def log_target(self, data, counts, locs, fluxes, temperature):
+        """sampler.py:87-91."""
+        logprior = self.Prior.log_prob(counts, locs, fluxes)
+        loglik = self.ImageModel.loglikelihood(data, locs, fluxes)
+        return logprior + temperature.unsqueeze(-1) * loglik
+
+    def tempering_objective(self, loglikelihood, delta):
+        """sampler.py:93-97 (host helper; temper() solves it on device)."""
+        log_numerator = 2 * ((delta * loglikelihood).logsumexp(0))
+        log_denominator = (2 * delta * loglikelihood).logsumexp(0)
+        return (log_numerator - log_denominator).exp() - self.ess_threshold
+
+    def _current_loglik(self):
+        if self._fresh_loglik is None:
+            self._fresh_loglik = self.ImageModel.loglikelihood(self.tiled_image, self.locs,
+                                                               self.fluxes)
+        return self._fresh_loglik
+
+    def temper(self):
+        """sampler.py:99-125, root-finding on device."""
+        self.loglik = self._current_loglik()
+        new_t = self.temperature.clone()
+        prev_t = torch.empty_like(new_t)
+        _hip.check(_hip.lib().smcdet_temper(
+            _hip.ptr(self.loglik), _hip.ptr(new_t), _hip.ptr(prev_t), self._T,
+            self.loglik.shape[-1], float(self.ess_threshold), _hip.stream_of(new_t)),
+            "smcdet_temper")
+        self.temperature_prev = prev_t
+        self.temperature = new_t
+
+    def update_weights(self):
+        """sampler.py:181-196."""
+        N = self.loglik.shape[-1]
+        self.weights_log_unnorm = torch.empty_like(self.loglik)
+        self.weights = torch.empty_like(self.loglik)
+        self.ess = torch.empty_like(self.temperature)
+        self.log_normalizing_constant = self.log_normalizing_constant.clone()
+        _hip.check(_hip.lib().smcdet_update_weights(
+            _hip.ptr(self.loglik), _hip.ptr(self.temperature), _hip.ptr(self.temperature_prev),
+            _hip.ptr(self.weights_log_unnorm), _hip.ptr(self.weights), _hip.ptr(self.ess),
+            _hip.ptr(self.log_normalizing_constant), self._T, N, _hip.stream_of(self.weights)),
+            "smcdet_update_weights")
+
+    def resample_index(self, u=None):
+        """Resampling indices [numH,numW,N] (sampler.py:128-150); u replays the
+        uniforms ([numH,numW] systematic, [numH,numW,N] multinomial)."""
+        N = self.weights.shape[-1]
+        idx = torch.empty(self.weights.shape, device=self.device, dtype=torch.int64)
+        off = self._resample_offset(N)
+        if u is not None:
+            u = _hip.dev_f32(u.to(self.device), "u")
+        _hip.check(_hip.lib().smcdet_resample_index(
+            _hip.ptr(self.weights), self._T, N, self._method_code(), self.rng.seed, off,
+            _hip.ptr(u), _hip.ptr(idx), _hip.stream_of(idx)), "smcdet_resample_index")
+        return idx
+
+    def _gather(self, idx):
+        N = idx.shape[-1]
+        S = self.locs.shape[-2]
+        c, l, f = (torch.empty_like(self.counts), torch.empty_like(self.locs),
+                   torch.empty_like(self.fluxes))
+        _hip.check(_hip.lib().smcdet_gather(
+            _hip.ptr(idx), self._T, N, S, _hip.ptr(self.counts), _hip.ptr(self.locs),
+            _hip.ptr(self.fluxes), _hip.ptr(c), _hip.ptr(l), _hip.ptr(f), _hip.stream_of(idx)),
+            "smcdet_gather")
+        self.counts, self.locs, self.fluxes = c, l, f
+        self.weights = torch.full_like(self.weights, 1.0 / N)
+        self._fresh_loglik = None
+
+    def resample(self):
+        """sampler.py:127-169."""
+        idx = self._pending_idx if self._pending_idx is not None else self.resample_index()
+        self._pending_idx = None
+        self._gather(idx)
+
+    def mutate(self, ancestors=None):
+        """sampler.py:171-179."""
+        self.locs, self.fluxes, self.mutation_acc_rates = self.MutationKernel.run(
+            self.tiled_image, self.counts, self.locs, self.fluxes, self.temperature,
+            self.log_target, ancestors=ancestors)
+        if ancestors is not None:
+            self.counts = self.MutationKernel.last_counts
+            self.weights = torch.full_like(self.weights, 1.0 / self.weights.shape[-1])
+        self._fresh_loglik = self.MutationKernel.last_loglik
+
+    def _temper_reweight(self, with_resample):
+        """temper + update_weights (+ next resampling indices), one launch."""
+        self.loglik = self._current_loglik()
+        N = self.loglik.shape[-1]
+        new_t = self.temperature.clone()
+        prev_t = torch.empty_like(new_t)
+        self.weights_log_unnorm = torch.empty_like(self.loglik)
+        self.weights = torch.empty_like(self.loglik)
+        self.ess = torch.empty_like(new_t)
+        self.log_normalizing_constant = self.log_normalizing_constant.clone()
+        idx = None
+        off = 0
+        if with_resample:
+            idx = torch.empty(self.loglik.shape, device=self.device, dtype=torch.int64)
+            off = self._resample_offset(N)
+        _hip.check(_hip.lib().smcdet_temper_reweight(
+            _hip.ptr(self.loglik), _hip.ptr(new_t), _hip.ptr(prev_t),
+            _hip.ptr(self.weights_log_unnorm), _hip.ptr(self.weights), _hip.ptr(self.ess),
+            _hip.ptr(self.log_normalizing_constant), self._T, N, float(self.ess_threshold),
+            self._method_code(), self.rng.seed, off, _hip.ptr(idx), _hip.stream_of(new_t)),
+            "smcdet_temper_reweight")
+        self.temperature_prev = prev_t
+        self.temperature = new_t
+        self._pending_idx = idx
+
+    def prune(self, locs, fluxes):
+        """sampler.py:198-219: detectable (flux > threshold) sources strictly
+        inside the tile, compacted to the front; counts int64."""
+        locs = _hip.dev_f32(locs, "locs")
+        fluxes = _hip.dev_f32(fluxes, "fluxes")
+        nH, nW, N, S, _ = locs.shape
+        counts = torch.empty(nH, nW, N, device=locs.device, dtype=torch.int64)
+        pl, pf = torch.empty_like(locs), torch.empty_like(fluxes)
+        _hip.check(_hip.lib().smcdet_prune(
+            _hip.ptr(locs), _hip.ptr(fluxes), nH * nW, N, S, float(self.tile_dim),
+            float(self.flux_detection_threshold), _hip.ptr(counts), _hip.ptr(pl), _hip.ptr(pf),
+            _hip.stream_of(locs)), "smcdet_prune")
+        return counts, pl, pf
+
+    def _print_progress(self):
+        if self.iter % self.print_every == 0:
+            acc = getattr(self, "mutation_acc_rates", None)
+            msg = (f"iteration {self.iter}: "
+                   f"temperature in [{round(self.temperature.min().item(), 2)}, "
+                   f"{round(self.temperature.max().item(), 2)}]")
+            if acc is not None:
+                msg += (f", acceptance rate in [{round(acc.min().item(), 2)}, "
+                        f"{round(acc.max().item(), 2)}]")
+            print(msg)
+
+    def run(self):
+        """sampler.py:221-256."""
+        self.iter = 0
+        print("starting...")
+        self.initialize()
+        if self.fused:
+            self._temper_reweight(with_resample=True)
+            while bool((self.temperature < 1).any()) and self.iter <= self.max_smc_iters:
+                self.iter += 1
+                self._print_progress()
+                idx, self._pending_idx = self._pending_idx, None
+                self.mutate(ancestors=idx)
+                self._temper_reweight(with_resample=True)
+        else:
+            self.temper()
+            self.update_weights()
+            while bool((self.temperature < 1).any()) and self.iter <= self.max_smc_iters:
+                self.iter += 1
+                self._print_progress()
+                self.resample()
+                self.mutate()
+                self.temper()
+                self.update_weights()
+        self.resample()
+        self.pruned_counts, self.pruned_locs, self.pruned_fluxes = self.prune(self.locs,
+                                                                              self.fluxes)
+        self.has_run = True
+        print("done!\n")
+
+    # ------------------------------------------------------------ summaries
+    def posterior_mean_count(self, counts):
+        return (self.weights * counts).sum(-1)
+
+    def posterior_mean_total_flux(self, fluxes):
+        return (self.weights * fluxes.sum(-1)).sum(-1)
+
+    @property
+    def posterior_predictive_total_observed_flux(self):
+        return self.ImageModel.sample(self.locs, self.fluxes).sum([-2, -3]).squeeze()
+
+    def summarize(self):
+        if self.has_run is False:
+            raise ValueError("Sampler hasn't been run yet.")
+        vals, cnts = self.pruned_counts.unique(return_counts=True)
+        print("posterior distribution of number of detectable stars within image boundary:")
+        print(vals.cpu())
+        print((cnts / self.pruned_counts.shape[-1]).round(decimals=3).cpu(), "\n")
+        print("posterior mean total intrinsic flux (including undetectable and/or in padding) =",
+              f"{self.posterior_mean_total_flux(self.fluxes).item()}\n")
+        print("posterior mean total intrinsic flux of detectable stars within image boundary =",
+              f"{self.posterior_mean_total_flux(self.pruned_fluxes).item()}\n")
+        print(f"number of unique catalogs = {self.fluxes[0, 0].sum(-1).unique(dim=0).shape[0]}")
+
+    # ------------------------------------------------------------ checkpoint
+    def state_dict(self):
+        """Sampler state for checkpoint / resume (tensors stay on device)."""
+        keys = ("counts", "locs", "fluxes", "weights", "weights_log_unnorm", "ess",
+                "log_normalizing_constant", "temperature", "temperature_prev", "loglik")
+        st = {k: getattr(self, k) for k in keys if hasattr(self, k)}
+        st["iter"] = getattr(self, "iter", 0)
+        st["rng"] = self.rng.state()
+        return st
+
+    def load_state_dict(self, st):
+        for k, v in st.items():
+            if k == "rng":
+                self.rng.load_state(v)
+            elif k == "iter":
+                self.iter = v
+            else:
+                setattr(self, k, v.to(self.device) if torch.is_tensor(v) else v)
+        self._fresh_loglik = st.get("loglik")
+        self._pending_idx = None

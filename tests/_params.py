@@ -86,3 +86,56 @@ def mh_fixture_setup(name):
 
 
 MH_FIXTURES = ["mh_m71_8x8", "mh_m71_32x32", "mh_m71_tiles", "mh_basic_16x16"]
+
+
+# ---- product-side constructors (smcdet_amd) -------------------------------
+def p_m71_model(H):
+    from smcdet_amd.images import M71ImageModel
+    p = M71
+    return M71ImageModel(image_height=H, image_width=H, background=p["background"],
+                         psf_radius=p["psf_radius"], adu_per_nmgy=p["adu_per_nmgy"],
+                         psf_params=p["psf_params"], noise_additive=p["noise_additive"],
+                         noise_multiplicative=p["noise_multiplicative"])
+
+
+def p_basic_model(H):
+    from smcdet_amd.images import ImageModel
+    return ImageModel(image_height=H, image_width=H, psf_radius=8, psf_stdev=BASIC_PSF_STDEV,
+                      background=BASIC_BACKGROUND)
+
+
+def p_m71_prior(H, smin, smax, counts_rate=M71["counts_rate"], pad=4):
+    from smcdet_amd.prior import M71Prior
+    p = M71
+    return M71Prior(min_objects=smin, max_objects=smax, counts_rate=counts_rate, image_height=H,
+                    image_width=H, flux_alpha=p["flux_alpha"], flux_lower=p["flux_lower"],
+                    flux_upper=p["flux_upper"], pad=pad)
+
+
+def p_basic_prior(H, smin, smax, pad=2):
+    from smcdet_amd.prior import ParetoStarPrior
+    return ParetoStarPrior(min_objects=smin, max_objects=smax, image_height=H, image_width=H,
+                           flux_scale=BASIC_FLUX_SCALE * 0.9, flux_alpha=BASIC_FLUX_ALPHA,
+                           pad=pad)
+
+
+def p_m71_mh(K, **kw):
+    from smcdet_amd.kernel import SingleComponentMH
+    return SingleComponentMH(K, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"], **kw)
+
+
+def p_basic_mh(K, **kw):
+    from smcdet_amd.kernel import SingleComponentMH
+    return SingleComponentMH(K, 0.1, 100, BASIC_FLUX_SCALE * 0.9, 1e6, **kw)
+
+
+def p_mh_fixture_setup(name, **kw):
+    if name == "mh_m71_8x8":
+        return 8, p_m71_model(8), p_m71_prior(8, 4, 4), p_m71_mh(20, **kw)
+    if name == "mh_m71_32x32":
+        return 32, p_m71_model(32), p_m71_prior(32, 10, 10), p_m71_mh(10, **kw)
+    if name == "mh_m71_tiles":
+        return 8, p_m71_model(8), p_m71_prior(8, 3, 3), p_m71_mh(10, **kw)
+    if name == "mh_basic_16x16":
+        return 16, p_basic_model(16), p_basic_prior(16, 3, 3), p_basic_mh(20, **kw)
+    raise KeyError(name)

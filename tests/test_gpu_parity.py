@@ -1,0 +1,280 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the golden
+vectors recorded from the reference and against the CPU oracle.
+
+Tolerances: the reference computes in float32; the kernels use float32
+arithmetic with float64 reductions, the oracle float64.  Log-likelihoods are
+compared with rtol 2e-6 (relative rounding of a 1,024-term float32 sum) plus
+an absolute floor; index work (resampling, pruning) must be bit-exact; MH
+replays must reproduce every accept decision of the reference.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import smc_oracle as O
+from tests._params import (M71, MH_FIXTURES, golden, mh_fixture_setup, o_m71_model,
+                           p_basic_model, p_basic_prior, p_m71_model, p_m71_mh, p_m71_prior,
+                           p_mh_fixture_setup, tiles_of)
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def T(x, dtype=torch.float32):
+    return torch.as_tensor(np.asarray(x)).to(DEV, dtype)
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+@pytest.mark.parametrize("H", [8, 16, 32])
+def test_psf_dense(H):
+    d = golden("psf.npz")
+    p = p_m71_model(H).psf(T(d[f"m71_H{H}_locs"]))
+    np.testing.assert_allclose(N(p), d[f"m71_H{H}_psf"], rtol=2e-6, atol=2e-8)
+    if H == 16:
+        p = p_basic_model(16).psf(T(d["m71_H16_locs"]))
+        np.testing.assert_allclose(N(p), d["basic_H16_psf"], rtol=2e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("key,H", [("m71_H8_S10", 8), ("m71_H32_S10", 32), ("m71_H16_S3", 16)])
+def test_loglik_m71_vs_reference(key, H):
+    d = golden("loglik.npz")
+    ll = p_m71_model(H).loglikelihood(T(d[key + "_image"])[None, None], T(d[key + "_locs"]),
+                                      T(d[key + "_fluxes"]))
+    np.testing.assert_allclose(N(ll), d[key + "_loglik_f64"], rtol=2e-6, atol=5e-3)
+    np.testing.assert_allclose(N(ll), d[key + "_loglik"], rtol=2e-6, atol=2e-2)
+    lp = p_m71_prior(H, 0, int(d[key + "_counts"].max())).log_prob(
+        T(d[key + "_counts"]), T(d[key + "_locs"]), T(d[key + "_fluxes"]))
+    np.testing.assert_allclose(N(lp), d[key + "_logprior"], rtol=1e-6, atol=1e-3)
+
+
+def test_loglik_tiles_and_poisson():
+    d = golden("loglik.npz")
+    ll = p_m71_model(8).loglikelihood(T(tiles_of(d["m71_tiles_image"], 8)),
+                                      T(d["m71_tiles_locs"]), T(d["m71_tiles_fluxes"]))
+    np.testing.assert_allclose(N(ll), d["m71_tiles_loglik"], rtol=2e-6, atol=2e-2)
+    for key in ("basic_H16_S3", "basic_bright"):
+        ll = p_basic_model(16).loglikelihood(T(d[key + "_image"])[None, None],
+                                             T(d[key + "_locs"]), T(d[key + "_fluxes"]))
+        np.testing.assert_allclose(N(ll), d[key + "_loglik"], rtol=2e-6, atol=2e-2)
+    lp = p_basic_prior(16, 3, 3).log_prob(T(d["basic_H16_S3_counts"]), T(d["basic_H16_S3_locs"]),
+                                          T(d["basic_H16_S3_fluxes"]))
+    np.testing.assert_allclose(N(lp), d["basic_H16_S3_logprior"], rtol=1e-6, atol=1e-3)
+
+
+def test_loglik_c2_scale_vs_oracle():
+    """C2 geometry (32x32, N=4096, S=10) against the float64 oracle."""
+    g = torch.Generator().manual_seed(5)
+    Np, S, H = 4096, 10, 32
+    locs = torch.rand(1, 1, Np, S, 2, generator=g) * 40 - 4
+    fl = M71["flux_lower"] + torch.rand(1, 1, Np, S, generator=g) ** 4 * 50
+    img = 104.15 + 14 * torch.randn(1, 1, H, H, generator=g)
+    ll = p_m71_model(H).loglikelihood(img.to(DEV), locs.to(DEV), fl.to(DEV))
+    ref = O.loglikelihood(img.numpy(), locs.numpy(), fl.numpy(), o_m71_model(H))
+    np.testing.assert_allclose(N(ll), ref, rtol=2e-6, atol=5e-3)
+
+
+def test_log_prior_counts_mask():
+    d = golden("prior.npz")
+    lp = p_m71_prior(8, 0, 12, counts_rate=0.01).log_prob(
+        T(d["m71_counts"]), T(d["m71_locs"]), T(d["m71_fluxes"]))
+    np.testing.assert_allclose(N(lp), d["m71_logprior"], rtol=1e-6, atol=1e-3)
+
+
+def test_prior_sample_replay():
+    d = golden("prior.npz")
+    pr = p_m71_prior(8, 3, 5)
+    c, l, f = pr.sample_stratified(2, 8, device=DEV, uloc=T(d["m71_strat_uloc"]),
+                                   uflux=T(d["m71_strat_uflux"]))
+    np.testing.assert_array_equal(N(c), d["m71_strat_counts"])
+    np.testing.assert_allclose(N(l), d["m71_strat_locs"], rtol=0, atol=4e-6)
+    np.testing.assert_allclose(N(f), d["m71_strat_fluxes"], rtol=4e-6, atol=0)
+
+
+def test_prior_sample_philox_statistics():
+    pr = p_m71_prior(32, 10, 10, counts_rate=0.003125)
+    torch.manual_seed(0)
+    c, l, f = pr.sample(num_tiles_per_side=2, stratify_by_count=True,
+                        num_catalogs_per_count=4096)
+    assert c.shape == (2, 2, 4096) and bool((c == 10).all())
+    lc = N(l)
+    assert lc.min() >= -4 and lc.max() < 36
+    assert abs(lc.mean() - 16.0) < 0.05
+    fc = N(f)
+    assert fc.min() >= np.float32(M71["flux_lower"]) and fc.max() <= np.float32(M71["flux_upper"])
+    # truncated-Pareto median check against the inverse CDF
+    med = O.trunc_pareto_sample(np.array([0.5]), M71["flux_alpha"], M71["flux_lower"],
+                                M71["flux_upper"])[0]
+    assert abs(np.median(fc) / med - 1) < 0.03
+
+
+def _mh_replay(name, full):
+    d = golden(name + ".npz")
+    td, model, prior, mh = p_mh_fixture_setup(name, full_recompute=full)
+    t = T(tiles_of(d["image"], td))
+    tau = T(np.full(t.shape[:2], float(d["tau"])))
+    mh.locs_min, mh.locs_max = torch.tensor(d["locs_min"]), torch.tensor(d["locs_max"])
+    replay = dict(comp=torch.as_tensor(d["comp"]), uloc=torch.as_tensor(d["uloc"]),
+                  uflux=torch.as_tensor(d["uflux"]), uacc=torch.as_tensor(d["uacc"]))
+    l, f, acc = mh.run(t, T(d["counts"]), T(d["locs0"]), T(d["fluxes0"]), tau, prior=prior,
+                       image_model=model, replay=replay)
+    return d, l, f, acc, mh
+
+
+@pytest.mark.parametrize("full", [False, True], ids=["incremental", "full"])
+@pytest.mark.parametrize("name", MH_FIXTURES)
+def test_mh_replay_vs_reference(name, full):
+    d, l, f, acc, mh = _mh_replay(name, full)
+    np.testing.assert_allclose(N(l), d["locs1"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(N(f), d["fluxes1"], rtol=2e-6, atol=1e-3)
+    np.testing.assert_array_equal(N(acc), d["acc"])
+    # the returned log-likelihood is that of the returned state
+    td, model, prior, _ = p_mh_fixture_setup(name)
+    ll = model.loglikelihood(T(tiles_of(d["image"], td)), l, f)
+    np.testing.assert_array_equal(N(mh.last_loglik), N(ll))
+
+
+def test_temper_update_weights_vs_reference():
+    from smcdet_amd import _hip
+    d = golden("smc_steps.npz")
+    ll = T(d["temper_loglik"])
+    tau = T(d["temper_tau_in"])
+    prev = torch.empty_like(tau)
+    _hip.check(_hip.lib().smcdet_temper(_hip.ptr(ll), _hip.ptr(tau), _hip.ptr(prev), 4, 512,
+                                        float(d["temper_rho_N"]), _hip.stream_of(ll)), "temper")
+    np.testing.assert_allclose(N(tau), d["temper_tau_out"], rtol=0, atol=2e-6)
+    np.testing.assert_array_equal(N(prev), d["temper_tau_in"])
+    lw, W = torch.empty_like(ll), torch.empty_like(ll)
+    ess = torch.empty_like(tau)
+    lz = T(d["weights_logZ_in"])
+    tout, tin = T(d["temper_tau_out"]), T(d["temper_tau_in"])
+    _hip.check(_hip.lib().smcdet_update_weights(
+        _hip.ptr(ll), _hip.ptr(tout), _hip.ptr(tin), _hip.ptr(lw), _hip.ptr(W), _hip.ptr(ess),
+        _hip.ptr(lz), 4, 512, _hip.stream_of(ll)), "update_weights")
+    np.testing.assert_allclose(N(W), d["weights_W"], rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(N(ess), d["weights_ess"], rtol=1e-5)
+    np.testing.assert_allclose(N(lz), d["weights_logZ"], rtol=1e-6, atol=1e-4)
+
+
+def _resample_idx(W, U):
+    from smcdet_amd import _hip
+    W = T(W)
+    nH, nW, Np = W.shape
+    idx = torch.empty(W.shape, device=DEV, dtype=torch.int64)
+    _hip.check(_hip.lib().smcdet_resample_index(
+        _hip.ptr(W), nH * nW, Np, _hip.SMCDET_RESAMPLE_SYSTEMATIC, 0, 0, _hip.ptr(T(U)),
+        _hip.ptr(idx), _hip.stream_of(W)), "resample_index")
+    return N(idx)
+
+
+def test_systematic_resample_bit_exact():
+    d = golden("smc_steps.npz")
+    np.testing.assert_array_equal(_resample_idx(d["resample_W"], d["resample_U"]),
+                                  d["resample_idx"])
+    np.testing.assert_array_equal(_resample_idx(d["resample_hand_W"], d["resample_hand_U"]),
+                                  d["resample_hand_idx"])
+    # larger random case against the oracle (float64 scan rounded per element)
+    rng = np.random.default_rng(3)
+    for Np in (1, 7, 4096, 10000):
+        w = rng.gamma(0.3, size=(2, 3, Np)).astype(np.float32)
+        W = (w / w.sum(-1, keepdims=True)).astype(np.float32)
+        U = rng.random((2, 3)).astype(np.float32)
+        np.testing.assert_array_equal(_resample_idx(W, U), O.systematic_resample_index(W, U))
+
+
+def test_multinomial_resample_distribution():
+    from smcdet_amd import _hip
+    Np = 4096
+    w = np.zeros((1, 1, Np), np.float32)
+    w[0, 0, :4] = [0.1, 0.2, 0.3, 0.4]
+    W = T(w)
+    idx = torch.empty(W.shape, device=DEV, dtype=torch.int64)
+    _hip.check(_hip.lib().smcdet_resample_index(
+        _hip.ptr(W), 1, Np, _hip.SMCDET_RESAMPLE_MULTINOMIAL, 1234, 0, None, _hip.ptr(idx),
+        _hip.stream_of(W)), "resample_index")
+    h = np.bincount(N(idx).ravel(), minlength=Np)
+    assert h[4:].sum() == 0
+    np.testing.assert_allclose(h[:4] / Np, [0.1, 0.2, 0.3, 0.4], atol=0.025)
+
+
+def test_prune_bit_exact():
+    from smcdet_amd.sampler import SMCsampler
+    d = golden("smc_steps.npz")
+    s = SMCsampler.__new__(SMCsampler)
+    s.tile_dim = int(d["prune_tile_dim"])
+    s.flux_detection_threshold = float(d["prune_threshold"])
+    pc, pl, pf = s.prune(T(d["prune_locs"]), T(d["prune_fluxes"]))
+    np.testing.assert_array_equal(N(pc), d["prune_counts"])
+    np.testing.assert_array_equal(N(pl), d["prune_out_locs"])
+    np.testing.assert_array_equal(N(pf), d["prune_out_fluxes"])
+
+
+def _replay_smc(d, fused_mh_gather):
+    """Drives smcdet_amd.SMCsampler method by method with the reference's
+    recorded draws (prior uniforms, systematic offsets, MH draws)."""
+    from smcdet_amd.sampler import SMCsampler
+    draws = O.DrawStream(d)
+    S, K, Np, td = int(d["S"]), int(d["K"]), int(d["N"]), int(d["tile_dim"])
+    prior, model, mh = p_m71_prior(td, S, S), p_m71_model(td), p_m71_mh(K)
+    s = SMCsampler(T(d["image"]), td, prior, model, mh, Np, 0.5, "systematic",
+                   M71["flux_detection_threshold"], 100, print_every=10 ** 9)
+    nt = s.num_tiles_per_side
+    uloc, uflux = draws.next("rand"), draws.next("rand")
+    s.counts, s.locs, s.fluxes = prior.sample_stratified(nt, Np, device=DEV, uloc=T(uloc),
+                                                         uflux=T(uflux))
+    s.temperature_prev = torch.zeros(nt, nt, device=DEV)
+    s.temperature = torch.zeros(nt, nt, device=DEV)
+    s.log_normalizing_constant = torch.zeros(nt, nt, device=DEV)
+    s._fresh_loglik = None
+    s.temper()
+    s.update_weights()
+    s.iter = 0
+    trace = [N(s.temperature)]
+    while bool((s.temperature < 1).any()) and s.iter <= s.max_smc_iters:
+        s.iter += 1
+        U = draws.next("rand")
+        idx = s.resample_index(u=T(U))
+        comp, ul, uf, ua = [], [], [], []
+        for _ in range(K):
+            m = draws.next("mask")
+            rl, rf, ra = draws.next("rand"), draws.next("rand"), draws.next("rand")
+            j = m.argmax(-1)
+            comp.append(j)
+            ul.append(np.take_along_axis(rl, j[..., None, None].repeat(2, -1), axis=-2)[..., 0, :])
+            uf.append(np.take_along_axis(rf, j[..., None], axis=-1)[..., 0])
+            ua.append(ra)
+        replay = dict(comp=torch.as_tensor(np.stack(comp)), uloc=torch.as_tensor(np.stack(ul)),
+                      uflux=torch.as_tensor(np.stack(uf)), uacc=torch.as_tensor(np.stack(ua)))
+        if fused_mh_gather:
+            anc = idx
+        else:
+            s._gather(idx)
+            anc = None
+        s.locs, s.fluxes, s.mutation_acc_rates = mh.run(
+            s.tiled_image, s.counts, s.locs, s.fluxes, s.temperature, s.log_target,
+            ancestors=anc, replay=replay)
+        if anc is not None:
+            s.counts = mh.last_counts
+        s._fresh_loglik = mh.last_loglik
+        s.temper()
+        s.update_weights()
+        trace.append(N(s.temperature))
+    U = draws.next("rand")
+    s._gather(s.resample_index(u=T(U)))
+    pc, pl, pf = s.prune(s.locs, s.fluxes)
+    return s, np.stack(trace), pc
+
+
+@pytest.mark.parametrize("fused", [False, True], ids=["gather", "mh-gather"])
+@pytest.mark.parametrize("name", ["smc_replay_m71_8x8", "smc_replay_m71_tiles"])
+def test_smc_end_to_end_replay_vs_reference(name, fused):
+    d = golden(name + ".npz")
+    s, trace, pc = _replay_smc(d, fused)
+    assert s.iter == int(d["iters"])
+    np.testing.assert_allclose(trace, d["trace_tau"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(N(s.log_normalizing_constant), d["logZ"], rtol=1e-5)
+    np.testing.assert_allclose(N(s.ess), d["ess"], rtol=1e-4)
+    np.testing.assert_allclose(N(s.locs), d["locs"], rtol=0, atol=2e-5)
+    np.testing.assert_array_equal(N(pc), d["pruned_counts"])

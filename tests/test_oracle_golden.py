@@ -170,3 +170,19 @@ def test_smc_end_to_end_replay(name):
     np.testing.assert_allclose(r["trace"]["tau"], d["trace_tau"], rtol=0, atol=1e-5)
     np.testing.assert_allclose(r["locs"], d["locs"], rtol=0, atol=2e-5)
     np.testing.assert_array_equal(r["pruned_counts"], d["pruned_counts"])
+
+
+@pytest.mark.parametrize("name", MH_FIXTURES)
+def test_c_oracle_mh_replay(name):
+    """The C restatement (bench.py's CPU baseline) replays the reference's
+    recorded MH draws to the same states and accept decisions."""
+    from oracle import c_oracle
+    d = golden(name + ".npz")
+    td, model, prior, mh = mh_fixture_setup(name)
+    t = tiles_of(d["image"], td)
+    replay = {k: d[k] for k in ("comp", "uloc", "uflux", "uacc")}
+    l, f, acc = c_oracle.mh_sweep(t, d["counts"], d["locs0"], d["fluxes0"], float(d["tau"]),
+                                  prior, model, mh, replay=replay, threads=2)
+    np.testing.assert_allclose(l, d["locs1"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(f, d["fluxes1"], rtol=1e-6, atol=5e-4)
+    np.testing.assert_array_equal(acc.astype(np.float32), d["acc"])
