@@ -113,7 +113,7 @@ def cpu_baseline(args, image_tile, seconds):
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     threads = max(1, min(threads, os.cpu_count() or 1))
     rng = np.random.default_rng(0)
-    n = max(64, 8 * threads)
+    n = max(64, 32 * threads)
     locs = (rng.random((1, 1, n, S, 2)) * (H + 8) - 4).astype(np.float32)
     fl = O.trunc_pareto_sample(rng.random((1, 1, n, S)), p["flux_alpha"], p["flux_lower"],
                                p["flux_upper"]).astype(np.float32)

@@ -157,6 +157,34 @@ __device__ __forceinline__ float pix_loglik(const DevModel& m, float x, float lg
   }
 }
 
+// log(1 + a), accurate for small |a| (Goldberg's trick on the hardware log2)
+__device__ __forceinline__ float log1p_fast(float a) {
+  const float u = 1.0f + a;
+  if (u == 1.0f) return a;
+  return kLn2 * fast_log2(u) * (a * fast_rcp(u - 1.0f));
+}
+
+// per-pixel log-likelihood CHANGE when the rate moves lam -> lam + dl, written
+// so that its relative error is that of the change (not of the two absolute
+// terms): M71  0.5*dl*(eta*d^2 + 2 d v - dl v)/(v v') - 0.5*log1p(eta dl / v),
+// d = x - lam, v = s0^2 + eta*lam;  Poisson  x*log1p(dl/lam) - dl.
+template <int MODEL>
+__device__ __forceinline__ float pix_delta(const DevModel& m, float x, float lgx, float lam,
+                                           float dl) {
+  const float lnew = lam + dl;
+  if constexpr (MODEL == SMCDET_MODEL_M71) {
+    const float v0 = fmaf(m.eta, lam, m.s0sq);
+    const float v1 = fmaf(m.eta, lnew, m.s0sq);
+    const float d0 = x - lam;
+    const float num = dl * (fmaf(m.eta * d0, d0, 2.0f * d0 * v0) - dl * v0);
+    return 0.5f * num * fast_rcp(v0 * v1) - 0.5f * log1p_fast(m.eta * dl * fast_rcp(v0));
+  } else {
+    if (lam > 50000.0f || lnew > 50000.0f)
+      return pix_loglik<MODEL>(m, x, lgx, lnew) - pix_loglik<MODEL>(m, x, lgx, lam);
+    return x * log1p_fast(dl * fast_rcp(lam)) - dl;
+  }
+}
+
 // Normal(mu, sigma).cdf(v) as torch computes it
 __device__ __forceinline__ float normal_cdf(float v, float mu, float inv_sigma) {
   return 0.5f * (1.0f + erff((v - mu) * inv_sigma * kSqrt1_2));

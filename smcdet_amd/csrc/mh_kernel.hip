@@ -5,8 +5,7 @@
 // One particle per 64-lane wavefront, 4 particles (of one tile) per 256-thread
 // workgroup sharing the tile image staged in LDS.  All K iterations run in one
 // launch; the particle's state lives in registers (lane s holds source s) and
-// its rate image lambda[H*W] plus the per-pixel log-likelihood terms live in
-// the wave's LDS slice.
+// its rate image lambda[H*W] lives in the wave's LDS slice.
 //
 // Per iteration (wave-uniform control):
 //   * draws: Philox4x32-10, 64 iterations at a time (lane i generates the 5
@@ -20,9 +19,10 @@
 //     source and dimension;
 //   * likelihood: only the moved source changes, so the delta log-likelihood
 //     is evaluated over the union of its old and new PSF windows (clipped to
-//     the tile, <= 18x18 positions for a step < 1 px): lambda' = lambda -
-//     g f psf_old + g f' psf_new per pixel, and the per-pixel term is
-//     re-evaluated there only.  (Mode SMCDET_MH_FULL_RECOMPUTE instead
+//     the tile, <= 18x18 positions for a step < 1 px): the rate changes by
+//     dl = g f' psf_new - g f psf_old there, and the per-pixel log-likelihood
+//     change is evaluated in a cancellation-free form (pix_delta, device.h)
+//     whose error scales with the change, not with the absolute terms.  (Mode SMCDET_MH_FULL_RECOMPUTE instead
 //     re-renders every source each step, as the reference does.)
 //   * accept iff U <= min(1, exp(log alpha)) (kernel.py:114-116).
 // The rate image is rebuilt from scratch at the start of each sweep and the
@@ -82,8 +82,7 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
   constexpr int kImg = (MODEL == SMCDET_MODEL_POISSON) ? 2 : 1;
   float* xs = smem;
   float* lg = smem + HW;
-  float* lam = smem + kImg * HW + wave * 2 * HW;
-  float* lp = lam + HW;
+  float* lam = smem + kImg * HW + wave * HW;
 
   stage_image<MODEL>(a.img + (size_t)t * HW, xs, lg, HW, threadIdx.x, kMhBlock);
   __syncthreads();
@@ -112,7 +111,7 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
 
   const float tau = a.temperature[t];
   render_sources<MODEL>(m, lam, sh, sw, sfx, S, lane);
-  double cur_ll = pixel_sum<MODEL>(m, xs, lg, lam, FULL ? nullptr : lp, lane);
+  double cur_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
 
   // lanes 0,1,2 handle proposal dimension d = h, w, flux
   const int d = lane < 3 ? lane : 2;
@@ -188,7 +187,7 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
     double new_ll = 0.0;
     const float amp_o = m.g * f, amp_n = m.g * fn;
     // register slots for the incremental path
-    float s_lam[kSlots], s_lp[kSlots];
+    float s_lam[kSlots];
     int s_pix[kSlots];
     int r0 = 0, c0 = 0, bw = 1, npos = 0;
     int fh0 = 0, fw0 = 0, fh1 = 0, fw1 = 0;
@@ -231,12 +230,11 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
               const float dh = fph - hn, dw = fpw - wn;
               psi_n = psf_eval<MODEL>(m, fmaf(dh, dh, dw * dw));
             }
-            const float lnew = fmaf(amp_n, psi_n, fmaf(-amp_o, psi_o, lam[p]));
+            const float dl = fmaf(amp_n, psi_n, -amp_o * psi_o);
+            const float lo = lam[p];
             const float lgx = (MODEL == SMCDET_MODEL_POISSON) ? lg[p] : 0.0f;
-            const float e = pix_loglik<MODEL>(m, xs[p], lgx, lnew);
-            dsum += e - lp[p];
-            s_lam[i] = lnew;
-            s_lp[i] = e;
+            dsum += pix_delta<MODEL>(m, xs[p], lgx, lo, dl);
+            s_lam[i] = lo + dl;
             s_pix[i] = p;
           }
         }
@@ -257,9 +255,9 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
           const float dh = fph - hn, dw = fpw - wn;
           psi_n = psf_eval<MODEL>(m, fmaf(dh, dh, dw * dw));
         }
-        const float lnew = fmaf(amp_n, psi_n, fmaf(-amp_o, psi_o, lam[p]));
+        const float dl = fmaf(amp_n, psi_n, -amp_o * psi_o);
         const float lgx = (MODEL == SMCDET_MODEL_POISSON) ? lg[p] : 0.0f;
-        dsum += pix_loglik<MODEL>(m, xs[p], lgx, lnew) - lp[p];
+        dsum += pix_delta<MODEL>(m, xs[p], lgx, lam[p], dl);
       }
       dll = wave_sum(dsum);
     }
@@ -277,7 +275,6 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
         for (int i = 0; i < kSlots; ++i) {
           if (i * kWave < npos && s_pix[i] >= 0) {
             lam[s_pix[i]] = s_lam[i];
-            lp[s_pix[i]] = s_lp[i];
           }
         }
         for (int q = kSlots * kWave + lane; q < npos; q += kWave) {
@@ -295,10 +292,7 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
             const float dh = fph - hn, dw = fpw - wn;
             psi_n = psf_eval<MODEL>(m, fmaf(dh, dh, dw * dw));
           }
-          const float lnew = fmaf(amp_n, psi_n, fmaf(-amp_o, psi_o, lam[p]));
-          const float lgx = (MODEL == SMCDET_MODEL_POISSON) ? lg[p] : 0.0f;
-          lam[p] = lnew;
-          lp[p] = pix_loglik<MODEL>(m, xs[p], lgx, lnew);
+          lam[p] += fmaf(amp_n, psi_n, -amp_o * psi_o);
         }
         cur_ll += (double)dll;
         wave_sync();
@@ -432,7 +426,7 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
     return set_error(SMCDET_EHIP, "smcdet_mh_sweep: memset failed");
   const size_t HW = (size_t)model->H * model->W;
   const size_t lds =
-      ((model->model == SMCDET_MODEL_POISSON ? 2 : 1) * HW + (size_t)kMhWaves * 2 * HW) *
+      ((model->model == SMCDET_MODEL_POISSON ? 2 : 1) * HW + (size_t)kMhWaves * HW) *
       sizeof(float);
   const dim3 grid((N + kMhWaves - 1) / kMhWaves, T);
   const bool full = (flags & SMCDET_MH_FULL_RECOMPUTE) != 0;
