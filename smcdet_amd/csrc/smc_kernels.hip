@@ -6,8 +6,9 @@
 // One 1024-thread workgroup per tile does temper -> reweight -> resample
 // indices in one launch, so an SMC iteration needs no host round trip (the
 // reference copies the log-likelihoods to the host and runs scipy brentq per
-// tile).  The tempering root is bracketed by a 17-ary search (16 waves each
-// evaluate ESS(delta) at one interior point per round) to |bracket| < 1e-12.
+// tile).  The tempering root is found by the same Brent iteration as scipy's
+// brentq (so the same root is picked when ESS(delta) crosses the threshold
+// more than once), each f evaluation being a workgroup-wide reduction.
 #include <math.h>
 
 #include "device.h"
@@ -61,29 +62,99 @@ __device__ float block_max(float v, float* redf) {
   return s;
 }
 
-// ESS(delta) - threshold evaluated by one wave over all N values:
-// ESS = (sum e)^2 / sum e^2,  e = exp(delta*(l - lmax))
-__device__ double wave_ess_objective(const float* ll, int N, float lmax, double delta,
-                                     double thr) {
-  const int lane = threadIdx.x & 63;
+// f(delta) = ESS(delta) - threshold, evaluated by the whole workgroup:
+// ESS = (sum e)^2 / sum e^2 with e = exp(d*l - max(d*l)), d = float32(delta)
+// (the reference multiplies its float32 log-likelihoods by the python float
+// delta, i.e. at float32 precision; sampler.py:93-97).  Sums in float64.
+__device__ double block_ess_objective(const float* ll, int N, float lmax, double delta,
+                                      double thr, double* red) {
   const float df = (float)delta;
+  const float m = df * lmax;  // = max_i fl(df*l_i): rounding is monotone
   double s1 = 0.0, s2 = 0.0;
-  for (int i = lane; i < N; i += kWave) {
-    const float e = expf(df * (ll[i] - lmax));
-    s1 += (double)e;
-    s2 += (double)e * (double)e;
+  for (int i = threadIdx.x; i < N; i += kTB) {
+    const double e = (double)expf(df * ll[i] - m);
+    s1 += e;
+    s2 += e * e;
   }
-  s1 = wave_sum(s1);
-  s2 = wave_sum(s2);
+  s1 = block_sum(s1, red);
+  s2 = block_sum(s2, red);
   return s1 * s1 / s2 - thr;
+}
+
+// scipy.optimize.brentq (scipy/optimize/Zeros/brentq.c, the algorithm the
+// reference calls at sampler.py:114-120) with xtol = rtol = 1e-6, maxiter
+// 100; thread 0 runs the control flow, the workgroup evaluates f.
+__device__ double block_brentq(const float* ll, int N, float lmax, double thr, double xa,
+                               double xb, double fa, double fb, double* red, double* sh) {
+  const double xtol = 1e-6, rtol = 1e-6;
+  // sh: [0]=next x, [1]=done flag, [2..]=solver state (thread 0 only)
+  double xpre = xa, xcur = xb, xblk = 0., fpre = fa, fcur = fb, fblk = 0., spre = 0., scur = 0.;
+  if (threadIdx.x == 0) {
+    sh[1] = 0.0;
+    if (fpre == 0.0) { sh[0] = xpre; sh[1] = 1.0; }
+    else if (fcur == 0.0) { sh[0] = xcur; sh[1] = 1.0; }
+  }
+  __syncthreads();
+  for (int it = 0; it < 100; ++it) {
+    if (threadIdx.x == 0 && sh[1] == 0.0) {
+      if (fpre != 0 && fcur != 0 && (signbit(fpre) != signbit(fcur))) {
+        xblk = xpre;
+        fblk = fpre;
+        spre = scur = xcur - xpre;
+      }
+      if (fabs(fblk) < fabs(fcur)) {
+        xpre = xcur; xcur = xblk; xblk = xpre;
+        fpre = fcur; fcur = fblk; fblk = fpre;
+      }
+      const double delta = (xtol + rtol * fabs(xcur)) / 2;
+      const double sbis = (xblk - xcur) / 2;
+      if (fcur == 0 || fabs(sbis) < delta) {
+        sh[0] = xcur;
+        sh[1] = 1.0;
+      } else {
+        if (fabs(spre) > delta && fabs(fcur) < fabs(fpre)) {
+          double stry;
+          if (xpre == xblk) {
+            stry = -fcur * (xcur - xpre) / (fcur - fpre);  // interpolate
+          } else {                                         // extrapolate
+            const double dpre = (fpre - fcur) / (xpre - xcur);
+            const double dblk = (fblk - fcur) / (xblk - xcur);
+            stry = -fcur * (fblk * dblk - fpre * dpre) / (dblk * dpre * (fblk - fpre));
+          }
+          if (2 * fabs(stry) < fmin(fabs(spre), 3 * fabs(sbis) - delta)) {
+            spre = scur;
+            scur = stry;
+          } else {
+            spre = sbis;
+            scur = sbis;
+          }
+        } else {
+          spre = sbis;
+          scur = sbis;
+        }
+        xpre = xcur;
+        fpre = fcur;
+        if (fabs(scur) > delta) xcur += scur;
+        else xcur += (sbis > 0 ? delta : -delta);
+        sh[0] = xcur;
+      }
+    }
+    __syncthreads();
+    if (sh[1] != 0.0) break;
+    const double fx = block_ess_objective(ll, N, lmax, sh[0], thr, red);
+    if (threadIdx.x == 0) fcur = fx;
+  }
+  __syncthreads();
+  const double root = sh[0];
+  __syncthreads();
+  return root;
 }
 
 __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
   extern __shared__ float bins[];  // N floats (resample only)
   __shared__ double red[kTW];
   __shared__ float redf[kTW];
-  __shared__ double fvals[kTW];
-  __shared__ double bracket[2];
+  __shared__ double bracket[4];
   const int t = blockIdx.x;
   const int N = a.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -96,42 +167,12 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
     for (int i = threadIdx.x; i < N; i += kTB) lm = fmaxf(lm, ll[i]);
     lm = block_max(lm, redf);
     const double top = 1.0 - (double)tau;
-    // f(top) by wave 0, broadcast through LDS
-    if (wave == 0) {
-      const double ftop = wave_ess_objective(ll, N, lm, top, a.ess_threshold);
-      if (lane == 0) {
-        bracket[0] = 0.0;
-        bracket[1] = ftop < 0.0 ? top : -1.0;  // -1 marks "no root needed"
-      }
-    }
-    __syncthreads();
-    double delta;
-    if (bracket[1] < 0.0) {
-      delta = top;
-    } else {
-      for (int round = 0; round < 40; ++round) {
-        const double lo = bracket[0], hi = bracket[1];
-        if (hi - lo <= 1e-12) break;
-        const double step = (hi - lo) / (double)(kTW + 1);
-        const double x = lo + step * (double)(wave + 1);
-        const double fx = wave_ess_objective(ll, N, lm, x, a.ess_threshold);
-        if (lane == 0) fvals[wave] = fx;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-          int first = kTW;  // first interior point with f < 0
-          for (int i = 0; i < kTW; ++i)
-            if (fvals[i] < 0.0) {
-              first = i;
-              break;
-            }
-          const double nlo = first == 0 ? lo : lo + step * (double)first;
-          const double nhi = first == kTW ? hi : lo + step * (double)(first + 1);
-          bracket[0] = nlo;
-          bracket[1] = nhi;
-        }
-        __syncthreads();
-      }
-      delta = 0.5 * (bracket[0] + bracket[1]);
+    // sampler.py:113-122: root-find only if ESS at delta = 1 - tau is below threshold
+    const double ftop = block_ess_objective(ll, N, lm, top, a.ess_threshold, red);
+    double delta = top;
+    if (ftop < 0.0) {
+      const double f0 = block_ess_objective(ll, N, lm, 0.0, a.ess_threshold, red);
+      delta = block_brentq(ll, N, lm, a.ess_threshold, 0.0, top, f0, ftop, red, bracket);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
