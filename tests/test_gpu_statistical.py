@@ -1,0 +1,112 @@
+"""Statistical parity of whole SMC runs against the reference.
+
+tests/golden/stats_{basic,m71}.json hold 20 seeded runs of the REFERENCE
+SMCsampler.run() (CPU, float32) on a fixed image (make_golden.py stats):
+  basic: 16x16 Poisson ImageModel + ParetoStarPrior(3,3), N=256, K=100, systematic
+  m71:   8x8 M71ImageModel + M71Prior(10,10), N=1000, K=100, systematic
+(make_golden.py passes the M71 flux_detection_threshold to both samplers.)
+Random streams cannot match torch's, so parity is distributional: mean log Z
+within 1% and within 3 pooled standard errors; non-final ESS = rho*N; final
+ESS, posterior mean total flux within 3 SE; pruned-count histogram total
+variation <= 0.05; SMC iteration counts within 3 SE.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests._params import (GOLDEN, M71, p_basic_mh, p_basic_model, p_basic_prior, p_m71_mh,
+                           p_m71_model, p_m71_prior)
+
+pytestmark = pytest.mark.gpu
+NSEEDS = 60
+
+
+def _load(which):
+    with open(os.path.join(GOLDEN, f"stats_{which}.json")) as f:
+        return json.load(f)
+
+
+def _run(which, cfg, image, seed, fused=True):
+    from smcdet_amd.sampler import SMCsampler
+    torch.manual_seed(seed)
+    H, N, S = cfg["tile"], cfg["N"], cfg["S"]
+    if which == "basic":
+        prior, model, mh = p_basic_prior(H, S, S), p_basic_model(H), p_basic_mh(cfg["K"])
+    else:
+        prior, model, mh = p_m71_prior(H, S, S), p_m71_model(H), p_m71_mh(cfg["K"])
+    s = SMCsampler(image, H, prior, model, mh, N, cfg["rho"], cfg["method"],
+                   M71["flux_detection_threshold"], 100, print_every=10 ** 9, fused=fused)
+    esses = []
+    orig = s._temper_reweight
+
+    def tr(with_resample, orig=orig):
+        orig(with_resample)
+        esses.append(float(s.ess.flatten()[0]))
+
+    s._temper_reweight = tr
+    s.run()
+    hist = np.bincount(s.pruned_counts.flatten().cpu().numpy(), minlength=S + 1)
+    return dict(logZ=float(s.log_normalizing_constant.flatten()[0]), iters=s.iter,
+                ess_trace=esses, final_ess=float(s.ess.flatten()[0]),
+                pruned_hist=hist / hist.sum(),
+                mean_total_flux=float(s.posterior_mean_total_flux(s.fluxes).flatten()[0]))
+
+
+def _se(a, b):
+    return np.sqrt(np.var(a, ddof=1) / len(a) + np.var(b, ddof=1) / len(b))
+
+
+@pytest.mark.parametrize("which", ["basic", "m71"])
+def test_statistical_parity_vs_reference(which):
+    ref = _load(which)
+    cfg = ref["config"]
+    image = torch.tensor(ref["image"], dtype=torch.float32, device="cuda")
+    runs = [_run(which, cfg, image, 1000 + i) for i in range(NSEEDS)]
+    rr = ref["runs"]
+    rho_n = cfg["rho"] * cfg["N"]
+
+    lz, lz_ref = np.array([r["logZ"] for r in runs]), np.array([r["logZ"] for r in rr])
+    se = _se(lz, lz_ref)
+    diff = lz.mean() - lz_ref.mean()
+    assert abs(diff) <= 3 * se, (which, lz.mean(), lz_ref.mean(), se)
+    assert abs(diff) <= 0.01 * abs(lz_ref.mean()), (which, lz.mean(), lz_ref.mean())
+
+    # every non-final tempering step lands on ESS = rho*N (root of the ESS equation)
+    for r in runs:
+        inner = np.array(r["ess_trace"][:-1])
+        np.testing.assert_allclose(inner, rho_n, rtol=0.01)
+
+    fe, fe_ref = np.array([r["final_ess"] for r in runs]), np.array([r["final_ess"] for r in rr])
+    assert abs(fe.mean() - fe_ref.mean()) <= 3 * _se(fe, fe_ref), (fe.mean(), fe_ref.mean())
+
+    it, it_ref = np.array([r["iters"] for r in runs]), np.array([r["iters"] for r in rr])
+    assert abs(it.mean() - it_ref.mean()) <= max(3 * _se(it, it_ref), 0.5), (it.mean(),
+                                                                             it_ref.mean())
+
+    fl = np.array([r["mean_total_flux"] for r in runs])
+    fl_ref = np.array([r["mean_total_flux"] for r in rr])
+    assert abs(fl.mean() - fl_ref.mean()) <= 3 * _se(fl, fl_ref), (fl.mean(), fl_ref.mean())
+
+    h = np.mean([r["pruned_hist"] for r in runs], axis=0)
+    h_ref = np.mean([r["pruned_hist"] for r in rr], axis=0)
+    n = max(len(h), len(h_ref))
+    h = np.pad(h, (0, n - len(h)))
+    h_ref = np.pad(h_ref, (0, n - len(h_ref)))
+    assert 0.5 * np.abs(h - h_ref).sum() <= 0.05, (h.round(3), h_ref.round(3))
+
+
+def test_fused_run_equals_method_by_method_run():
+    """run() with the fused schedule (MH gathers the ancestors; one per-tile
+    launch does temper + reweight + next resampling indices) consumes the
+    random streams in the same order as the method-by-method schedule."""
+    ref = _load("basic")
+    cfg = ref["config"]
+    image = torch.tensor(ref["image"], dtype=torch.float32, device="cuda")
+    a = _run("basic", cfg, image, 7, fused=True)
+    b = _run("basic", cfg, image, 7, fused=False)
+    assert a["iters"] == b["iters"]
+    assert a["logZ"] == b["logZ"]
+    np.testing.assert_array_equal(a["pruned_hist"], b["pruned_hist"])
