@@ -1,0 +1,27 @@
+#!/bin/bash
+# rocprofv3 kernel trace + stats of the bench, then separate PMC passes for the
+# MH kernel (counter passes never combined with other trace domains).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/prof
+mkdir -p $OUT
+B="bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-}"
+run() {  # $1 = name, rest = rocprofv3 args
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 "$@" -T -f csv -d $OUT/$name -o run -- python3 $B > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+if [ "${LIST:-0}" = "1" ]; then
+  timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "list rc=$?"
+fi
+if [ "${TRACE:-1}" = "1" ]; then
+  run trace --kernel-trace --stats
+  run fetch --pmc FETCH_SIZE --kernel-include-regex mh_sweep
+  run write --pmc WRITE_SIZE --kernel-include-regex mh_sweep
+fi
+if [ -n "${SQ:-}" ]; then run sq --pmc $SQ --kernel-include-regex mh_sweep; fi
+if [ -n "${SQ2:-}" ]; then run sq2 --pmc $SQ2 --kernel-include-regex mh_sweep; fi
+if [ -n "${SQ3:-}" ]; then run sq3 --pmc $SQ3 --kernel-include-regex mh_sweep; fi

@@ -82,20 +82,61 @@ __device__ __forceinline__ int readlane(int v, int lane) {
   return __builtin_amdgcn_readlane(v, lane);
 }
 
+// 64-lane reductions on DPP (no LDS crossbar round trips): quad_perm
+// [1,0,3,2], [2,3,0,1], row_shr:4, row_shr:8 leave each row's sum in its lane
+// 15; row_bcast:15 (rows 1,3) and row_bcast:31 (rows 2,3) fold the rows into
+// lane 63, which is broadcast with v_readlane.  Call from converged code.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ int dpp_move(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xf, false);
+}
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(dpp_move<CTRL, ROW_MASK>(__float_as_int(v)));
+}
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = dpp_move<CTRL, ROW_MASK>((int)(b & 0xffffffffll));
+  const int hi = dpp_move<CTRL, ROW_MASK>((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
+  v += dpp_f<0xb1>(v);
+  v += dpp_f<0x4e>(v);
+  v += dpp_f<0x114>(v);
+  v += dpp_f<0x118>(v);
+  v += dpp_f<0x142, 0xa>(v);
+  v += dpp_f<0x143, 0xc>(v);
+  return readlane(v, 63);
 }
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
+  v += dpp_d<0xb1>(v);
+  v += dpp_d<0x4e>(v);
+  v += dpp_d<0x114>(v);
+  v += dpp_d<0x118>(v);
+  v += dpp_d<0x142, 0xa>(v);
+  v += dpp_d<0x143, 0xc>(v);
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// max: out-of-row sources read the identity, so use -inf as `old`
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_fmax(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-INFINITY), __float_as_int(v),
+                                                    CTRL, ROW_MASK, 0xf, false));
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
-  return v;
+  v = fmaxf(v, dpp_fmax<0xb1>(v));
+  v = fmaxf(v, dpp_fmax<0x4e>(v));
+  v = fmaxf(v, dpp_fmax<0x114>(v));
+  v = fmaxf(v, dpp_fmax<0x118>(v));
+  v = fmaxf(v, dpp_fmax<0x142, 0xa>(v));
+  v = fmaxf(v, dpp_fmax<0x143, 0xc>(v));
+  return readlane(v, 63);
 }
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -185,9 +226,60 @@ __device__ __forceinline__ float pix_delta(const DevModel& m, float x, float lgx
   }
 }
 
-// Normal(mu, sigma).cdf(v) as torch computes it
+__device__ __forceinline__ float fast_exp(float x) { return fast_exp2(x * kLog2e); }
+__device__ __forceinline__ float fast_log(float x) { return kLn2 * fast_log2(x); }
+
+// erfc(|x|) with fractional error < 1.2e-7 everywhere (Numerical Recipes'
+// Chebyshev fit), branch-free
+__device__ __forceinline__ float erfc_abs(float x) {
+  const float z = fabsf(x);
+  const float t = fast_rcp(fmaf(0.5f, z, 1.0f));
+  float p = 0.17087277f;
+  p = fmaf(p, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  p = fmaf(p, t, -1.26551223f);
+  return t * fast_exp(fmaf(-z, z, p));
+}
+
+// Normal(mu, sigma).cdf(v) = 0.5 erfc(-(v-mu)/(sigma sqrt2)); accurate in both
+// tails (the reference's 0.5(1+erf) form has only absolute accuracy there)
 __device__ __forceinline__ float normal_cdf(float v, float mu, float inv_sigma) {
-  return 0.5f * (1.0f + erff((v - mu) * inv_sigma * kSqrt1_2));
+  const float u = (v - mu) * inv_sigma * kSqrt1_2;
+  const float e = 0.5f * erfc_abs(u);
+  return u < 0.f ? e : 1.0f - e;
+}
+
+// inverse error function (Giles 2010, single precision, |rel err| < 4e-7),
+// both branches evaluated (branch-free across the lanes that call it)
+__device__ __forceinline__ float erfinv_fast(float x) {
+  float w = -fast_log((1.0f - x) * (1.0f + x));
+  const float wa = w - 2.5f;
+  float pa = 2.81022636e-08f;
+  pa = fmaf(pa, wa, 3.43273939e-07f);
+  pa = fmaf(pa, wa, -3.5233877e-06f);
+  pa = fmaf(pa, wa, -4.39150654e-06f);
+  pa = fmaf(pa, wa, 0.00021858087f);
+  pa = fmaf(pa, wa, -0.00125372503f);
+  pa = fmaf(pa, wa, -0.00417768164f);
+  pa = fmaf(pa, wa, 0.246640727f);
+  pa = fmaf(pa, wa, 1.50140941f);
+  const float wb = sqrtf(w) - 3.0f;
+  float pb = -0.000200214257f;
+  pb = fmaf(pb, wb, 0.000100950558f);
+  pb = fmaf(pb, wb, 0.00134934322f);
+  pb = fmaf(pb, wb, -0.00367342844f);
+  pb = fmaf(pb, wb, 0.00573950773f);
+  pb = fmaf(pb, wb, -0.0076224613f);
+  pb = fmaf(pb, wb, 0.00943887047f);
+  pb = fmaf(pb, wb, 1.00167406f);
+  pb = fmaf(pb, wb, 2.83297682f);
+  return (w < 5.0f ? pa : pb) * x;
 }
 
 struct DevPrior {

@@ -69,7 +69,7 @@ __device__ __forceinline__ void tn_cache(float mu, float isig, float lb, float u
                                          float& Z, float& lZ) {
   phl = normal_cdf(lb, mu, isig);
   Z = normal_cdf(ub, mu, isig) - phl;
-  lZ = nan_to_num(logf(Z), 0.0f);
+  lZ = nan_to_num(fast_log(Z), 0.0f);
 }
 
 template <int MODEL, bool REPLAY, bool FULL>
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
   tn_cache(sh, a.isl, a.lb_h, a.ub_h, ph_h, Z_h, lZ_h);
   tn_cache(sw, a.isl, a.lb_w, a.ub_w, ph_w, Z_w, lZ_w);
   tn_cache(sfx, a.isf, a.lb_f, a.ub_f, ph_f, Z_f, lZ_f);
-  float lfx = logf(sfx);
+  float lfx = fast_log(sfx);
 
   const float tau = a.temperature[t];
   render_sources<MODEL>(m, lam, sh, sw, sfx, S, lane);
@@ -167,14 +167,14 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
 
     // ---- truncated-normal proposal, lanes 0..2 (distributions.py:40-48) ------
     const float pc = fminf(fmaxf(u, 1e-6f), 0.999999f);
-    float pt = c_ph + pc * expf(c_lZ);
+    float pt = c_ph + pc * fast_exp(c_lZ);
     pt = fminf(fmaxf(pt, 1e-6f), 0.999999f);
-    float xn = mu + p_sig * erfinvf(2.0f * pt - 1.0f) * kSqrt2;
+    float xn = mu + p_sig * erfinv_fast(2.0f * pt - 1.0f) * kSqrt2;
     xn = fminf(fmaxf(xn, p_lb), p_ub);
     float n_ph, n_Z, n_lZ;
     tn_cache(xn, p_isig, p_lb, p_ub, n_ph, n_Z, n_lZ);
     const float hast_d = c_lZ - n_lZ;  // log q(z|z') - log q(z'|z), this dimension
-    const float n_lf = logf(xn);
+    const float n_lf = fast_log(xn);
 
     const float hn = readlane(xn, 0), wn = readlane(xn, 1), fn = readlane(xn, 2);
     const float hast = readlane(hast_d, 0) + readlane(hast_d, 1) + readlane(hast_d, 2);
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
 
     // ---- accept / reject (kernel.py:114-128) ----------------------------------
     const float loga = dprior + tau * dll + hast;
-    const float e = expf(loga);
+    const float e = fast_exp(loga);
     const float alpha = e > 1.0f ? 1.0f : e;  // clamp(max=1) keeps NaN
     accept = uacc <= alpha;
     if (accept) {

@@ -62,12 +62,38 @@ __device__ float block_max(float v, float* redf) {
   return s;
 }
 
+// two block sums with ONE barrier: wave DPP sums -> per-wave slots of a
+// double-buffered LDS array -> every thread adds the 16 slots in a fixed
+// order (deterministic, and every thread ends with the same value)
+struct Red2 {
+  double v[2][kTW][2];
+};
+__device__ __forceinline__ void block_sum2(double& a, double& b, Red2* r, int& parity) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int k = parity;
+  parity ^= 1;  // every thread toggles identically: the next call uses the other buffer
+  if (lane == 0) {
+    r->v[k][wave][0] = a;
+    r->v[k][wave][1] = b;
+  }
+  __syncthreads();
+  double sa = 0.0, sb = 0.0;
+  for (int i = 0; i < kTW; ++i) {
+    sa += r->v[k][i][0];
+    sb += r->v[k][i][1];
+  }
+  a = sa;
+  b = sb;
+}
+
 // f(delta) = ESS(delta) - threshold, evaluated by the whole workgroup:
 // ESS = (sum e)^2 / sum e^2 with e = exp(d*l - max(d*l)), d = float32(delta)
 // (the reference multiplies its float32 log-likelihoods by the python float
 // delta, i.e. at float32 precision; sampler.py:93-97).  Sums in float64.
 __device__ double block_ess_objective(const float* ll, int N, float lmax, double delta,
-                                      double thr, double* red) {
+                                      double thr, Red2* red, int& parity) {
   const float df = (float)delta;
   const float m = df * lmax;  // = max_i fl(df*l_i): rounding is monotone
   double s1 = 0.0, s2 = 0.0;
@@ -76,85 +102,68 @@ __device__ double block_ess_objective(const float* ll, int N, float lmax, double
     s1 += e;
     s2 += e * e;
   }
-  s1 = block_sum(s1, red);
-  s2 = block_sum(s2, red);
+  block_sum2(s1, s2, red, parity);
   return s1 * s1 / s2 - thr;
 }
 
 // scipy.optimize.brentq (scipy/optimize/Zeros/brentq.c, the algorithm the
 // reference calls at sampler.py:114-120) with xtol = rtol = 1e-6, maxiter
-// 100; thread 0 runs the control flow, the workgroup evaluates f.
+// 100.  Every thread runs the (deterministic) control flow on identical
+// values; the workgroup evaluates f together.
 __device__ double block_brentq(const float* ll, int N, float lmax, double thr, double xa,
-                               double xb, double fa, double fb, double* red, double* sh) {
+                               double xb, double fa, double fb, Red2* red, int& parity) {
   const double xtol = 1e-6, rtol = 1e-6;
-  // sh: [0]=next x, [1]=done flag, [2..]=solver state (thread 0 only)
   double xpre = xa, xcur = xb, xblk = 0., fpre = fa, fcur = fb, fblk = 0., spre = 0., scur = 0.;
-  if (threadIdx.x == 0) {
-    sh[1] = 0.0;
-    if (fpre == 0.0) { sh[0] = xpre; sh[1] = 1.0; }
-    else if (fcur == 0.0) { sh[0] = xcur; sh[1] = 1.0; }
-  }
-  __syncthreads();
+  if (fpre == 0.0) return xpre;
+  if (fcur == 0.0) return xcur;
   for (int it = 0; it < 100; ++it) {
-    if (threadIdx.x == 0 && sh[1] == 0.0) {
-      if (fpre != 0 && fcur != 0 && (signbit(fpre) != signbit(fcur))) {
-        xblk = xpre;
-        fblk = fpre;
-        spre = scur = xcur - xpre;
-      }
-      if (fabs(fblk) < fabs(fcur)) {
-        xpre = xcur; xcur = xblk; xblk = xpre;
-        fpre = fcur; fcur = fblk; fblk = fpre;
-      }
-      const double delta = (xtol + rtol * fabs(xcur)) / 2;
-      const double sbis = (xblk - xcur) / 2;
-      if (fcur == 0 || fabs(sbis) < delta) {
-        sh[0] = xcur;
-        sh[1] = 1.0;
-      } else {
-        if (fabs(spre) > delta && fabs(fcur) < fabs(fpre)) {
-          double stry;
-          if (xpre == xblk) {
-            stry = -fcur * (xcur - xpre) / (fcur - fpre);  // interpolate
-          } else {                                         // extrapolate
-            const double dpre = (fpre - fcur) / (xpre - xcur);
-            const double dblk = (fblk - fcur) / (xblk - xcur);
-            stry = -fcur * (fblk * dblk - fpre * dpre) / (dblk * dpre * (fblk - fpre));
-          }
-          if (2 * fabs(stry) < fmin(fabs(spre), 3 * fabs(sbis) - delta)) {
-            spre = scur;
-            scur = stry;
-          } else {
-            spre = sbis;
-            scur = sbis;
-          }
-        } else {
-          spre = sbis;
-          scur = sbis;
-        }
-        xpre = xcur;
-        fpre = fcur;
-        if (fabs(scur) > delta) xcur += scur;
-        else xcur += (sbis > 0 ? delta : -delta);
-        sh[0] = xcur;
-      }
+    if (fpre != 0 && fcur != 0 && (signbit(fpre) != signbit(fcur))) {
+      xblk = xpre;
+      fblk = fpre;
+      spre = scur = xcur - xpre;
     }
-    __syncthreads();
-    if (sh[1] != 0.0) break;
-    const double fx = block_ess_objective(ll, N, lmax, sh[0], thr, red);
-    if (threadIdx.x == 0) fcur = fx;
+    if (fabs(fblk) < fabs(fcur)) {
+      xpre = xcur; xcur = xblk; xblk = xpre;
+      fpre = fcur; fcur = fblk; fblk = fpre;
+    }
+    const double delta = (xtol + rtol * fabs(xcur)) / 2;
+    const double sbis = (xblk - xcur) / 2;
+    if (fcur == 0 || fabs(sbis) < delta) return xcur;
+    if (fabs(spre) > delta && fabs(fcur) < fabs(fpre)) {
+      double stry;
+      if (xpre == xblk) {
+        stry = -fcur * (xcur - xpre) / (fcur - fpre);  // interpolate
+      } else {                                         // extrapolate
+        const double dpre = (fpre - fcur) / (xpre - xcur);
+        const double dblk = (fblk - fcur) / (xblk - xcur);
+        stry = -fcur * (fblk * dblk - fpre * dpre) / (dblk * dpre * (fblk - fpre));
+      }
+      if (2 * fabs(stry) < fmin(fabs(spre), 3 * fabs(sbis) - delta)) {
+        spre = scur;
+        scur = stry;
+      } else {
+        spre = sbis;
+        scur = sbis;
+      }
+    } else {
+      spre = sbis;
+      scur = sbis;
+    }
+    xpre = xcur;
+    fpre = fcur;
+    if (fabs(scur) > delta) xcur += scur;
+    else xcur += (sbis > 0 ? delta : -delta);
+    fcur = block_ess_objective(ll, N, lmax, xcur, thr, red, parity);
   }
-  __syncthreads();
-  const double root = sh[0];
-  __syncthreads();
-  return root;
+  return xcur;
 }
 
 __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
   extern __shared__ float bins[];  // N floats (resample only)
   __shared__ double red[kTW];
   __shared__ float redf[kTW];
-  __shared__ double bracket[4];
+  __shared__ Red2 red2;
+  int parity = 0;
   const int t = blockIdx.x;
   const int N = a.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -168,11 +177,11 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
     lm = block_max(lm, redf);
     const double top = 1.0 - (double)tau;
     // sampler.py:113-122: root-find only if ESS at delta = 1 - tau is below threshold
-    const double ftop = block_ess_objective(ll, N, lm, top, a.ess_threshold, red);
+    const double ftop = block_ess_objective(ll, N, lm, top, a.ess_threshold, &red2, parity);
     double delta = top;
     if (ftop < 0.0) {
-      const double f0 = block_ess_objective(ll, N, lm, 0.0, a.ess_threshold, red);
-      delta = block_brentq(ll, N, lm, a.ess_threshold, 0.0, top, f0, ftop, red, bracket);
+      const double f0 = block_ess_objective(ll, N, lm, 0.0, a.ess_threshold, &red2, parity);
+      delta = block_brentq(ll, N, lm, a.ess_threshold, 0.0, top, f0, ftop, &red2, parity);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
