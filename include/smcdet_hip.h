@@ -49,6 +49,9 @@ extern "C" {
 
 /* mh flags */
 #define SMCDET_MH_FULL_RECOMPUTE 1u /* re-render every source per step (reference arithmetic) */
+/* diagnostic ablations (timing only; results are NOT valid samples) */
+#define SMCDET_MH_ABLATE_LIKELIHOOD 256u /* skip the delta-likelihood passes */
+#define SMCDET_MH_ABLATE_PROPOSAL 512u   /* skip the truncated-normal proposal math */
 
 /* Image model (smcdet/images.py:6-26 ImageModel, :105-145 M71ImageModel). */
 typedef struct smcdet_image_model {

@@ -1,0 +1,97 @@
+#!/usr/bin/env python
+"""Interleaved A/B timing of MH-sweep variants at the C2 geometry (one
+process, rounds interleaved; reports median and min ms per launch).
+
+Variants: incremental (default), the diagnostic ablations
+(SMCDET_MH_ABLATE_LIKELIHOOD / _PROPOSAL: timing only), full recompute, and
+the per-tile temper+reweight+resample launch."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from smcdet_amd import _hip  # noqa: E402
+from tests._params import M71, p_m71_mh, p_m71_model, p_m71_prior  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--particles", type=int, default=4096)
+    ap.add_argument("--tiles", type=int, default=1)
+    ap.add_argument("--K", type=int, default=100)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--full", action="store_true", help="include the full-recompute variant")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    H, S, Np = 32, 10, a.particles
+    nt = int(round(a.tiles ** 0.5))
+    model, prior = p_m71_model(H), p_m71_prior(H, S, S, counts_rate=0.003125)
+    truth = p_m71_prior(H, 0, 100, counts_rate=0.003125)
+    img = torch.empty(nt, nt, H, H, device=dev)
+    for i in range(nt):
+        for j in range(nt):
+            while True:
+                c, l, f = truth.sample(num_catalogs=1, device=dev)
+                if int(c.max()) <= S:
+                    break
+            img[i, j] = model.sample(l, f)[0, 0, :, :, 0]
+    counts, locs, fluxes = prior.sample(num_tiles_per_side=nt, stratify_by_count=True,
+                                        num_catalogs_per_count=Np, device=dev)
+    tau = torch.full((nt, nt), 0.3, device=dev)
+    variants = {"incremental": (False, 0),
+                "no_likelihood": (False, _hip.SMCDET_MH_ABLATE_LIKELIHOOD if hasattr(
+                    _hip, "SMCDET_MH_ABLATE_LIKELIHOOD") else 256),
+                "no_proposal": (False, 512),
+                "no_both": (False, 768)}
+    if a.full:
+        variants["full_recompute"] = (True, 0)
+    times = {k: [] for k in variants}
+    times["tile_kernel"] = []
+    mhs = {}
+    for k, (full, fl) in variants.items():
+        mh = p_m71_mh(a.K, full_recompute=full)
+        mh.debug_flags = fl
+        mhs[k] = mh
+    ll = model.loglikelihood(img, locs, fluxes)
+    for r in range(a.rounds + 1):
+        for k, mh in mhs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            mh.run(img, counts, locs, fluxes, tau, prior=prior, image_model=model)
+            e1.record()
+            torch.cuda.synchronize()
+            if r:
+                times[k].append(e0.elapsed_time(e1))
+        # the per-tile launch
+        T = nt * nt
+        t_ = torch.zeros(T, device=dev)
+        tp, lw, W = torch.empty(T, device=dev), torch.empty_like(ll), torch.empty_like(ll)
+        ess, lz = torch.empty(T, device=dev), torch.zeros(T, device=dev)
+        idx = torch.empty(ll.shape, device=dev, dtype=torch.int64)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _hip.check(_hip.lib().smcdet_temper_reweight(
+            _hip.ptr(ll), _hip.ptr(t_), _hip.ptr(tp), _hip.ptr(lw), _hip.ptr(W), _hip.ptr(ess),
+            _hip.ptr(lz), T, Np, 0.5 * Np, 1, 1, 0, _hip.ptr(idx), _hip.stream_of(ll)), "tr")
+        e1.record()
+        torch.cuda.synchronize()
+        if r:
+            times["tile_kernel"].append(e0.elapsed_time(e1))
+    out = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))}
+           for k, v in times.items()}
+    steps = nt * nt * Np * a.K
+    for k, v in out.items():
+        if k != "tile_kernel":
+            v["particle_steps_per_s"] = steps / (v["median_ms"] * 1e-3)
+    print(json.dumps({"config": vars(a), "variants": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -46,6 +46,7 @@ struct MhArgs {
   float lb_f, ub_f;                  // flux box
   uint32_t k0, k1;                   // Philox key (seed)
   uint64_t offset;                   // Philox counter base (iterations)
+  uint32_t ablate;                   // SMCDET_MH_ABLATE_* (diagnostics)
   const float* img;                  // [T,H,W]
   const float* temperature;          // [T]
   const int64_t* ancestors;          // [T,N] or null
@@ -166,15 +167,25 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
     const float u = d == 0 ? readlane(ru1, kl) : (d == 1 ? readlane(ru2, kl) : readlane(ru3, kl));
 
     // ---- truncated-normal proposal, lanes 0..2 (distributions.py:40-48) ------
-    const float pc = fminf(fmaxf(u, 1e-6f), 0.999999f);
-    float pt = c_ph + pc * fast_exp(c_lZ);
-    pt = fminf(fmaxf(pt, 1e-6f), 0.999999f);
-    float xn = mu + p_sig * erfinv_fast(2.0f * pt - 1.0f) * kSqrt2;
-    xn = fminf(fmaxf(xn, p_lb), p_ub);
-    float n_ph, n_Z, n_lZ;
-    tn_cache(xn, p_isig, p_lb, p_ub, n_ph, n_Z, n_lZ);
-    const float hast_d = c_lZ - n_lZ;  // log q(z|z') - log q(z'|z), this dimension
-    const float n_lf = fast_log(xn);
+    float xn, n_ph, n_Z, n_lZ, hast_d, n_lf;
+    if (a.ablate & SMCDET_MH_ABLATE_PROPOSAL) {
+      // timing-only stand-in: a small deterministic move, no special functions
+      xn = fminf(fmaxf(mu + (u - 0.5f) * p_sig, p_lb), p_ub);
+      n_ph = c_ph;
+      n_Z = 1.f;
+      n_lZ = c_lZ;
+      hast_d = 0.f;
+      n_lf = xn;
+    } else {
+      const float pc = fminf(fmaxf(u, 1e-6f), 0.999999f);
+      float pt = c_ph + pc * fast_exp(c_lZ);
+      pt = fminf(fmaxf(pt, 1e-6f), 0.999999f);
+      xn = mu + p_sig * erfinv_fast(2.0f * pt - 1.0f) * kSqrt2;
+      xn = fminf(fmaxf(xn, p_lb), p_ub);
+      tn_cache(xn, p_isig, p_lb, p_ub, n_ph, n_Z, n_lZ);
+      hast_d = c_lZ - n_lZ;  // log q(z|z') - log q(z'|z), this dimension
+      n_lf = fast_log(xn);
+    }
 
     const float hn = readlane(xn, 0), wn = readlane(xn, 1), fn = readlane(xn, 2);
     const float hast = readlane(hast_d, 0) + readlane(hast_d, 1) + readlane(hast_d, 2);
@@ -207,7 +218,8 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
       c0 = max(min(fw0, fw1) - m.R, 0);
       const int c1 = min(max(fw0, fw1) + m.R, m.W - 1);
       bw = c1 - c0 + 1;
-      npos = (r1 >= r0 && c1 >= c0) ? (r1 - r0 + 1) * bw : 0;
+      npos = (r1 >= r0 && c1 >= c0 && !(a.ablate & SMCDET_MH_ABLATE_LIKELIHOOD))
+                 ? (r1 - r0 + 1) * bw : 0;
       inv_bw = 1.0f / (float)bw;
       float dsum = 0.f;
 #pragma unroll
@@ -430,6 +442,7 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
       sizeof(float);
   const dim3 grid((N + kMhWaves - 1) / kMhWaves, T);
   const bool full = (flags & SMCDET_MH_FULL_RECOMPUTE) != 0;
+  a.ablate = flags & (SMCDET_MH_ABLATE_LIKELIHOOD | SMCDET_MH_ABLATE_PROPOSAL);
   rc = a.m.model == SMCDET_MODEL_M71
            ? launch_mh<SMCDET_MODEL_M71>(a, replay != nullptr, full, grid, lds, st)
            : launch_mh<SMCDET_MODEL_POISSON>(a, replay != nullptr, full, grid, lds, st);

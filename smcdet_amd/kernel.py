@@ -37,6 +37,7 @@ class SingleComponentMH(object):
         # False: incremental delta log-likelihood over the moved source's windows
         self.full_recompute = full_recompute
         self.rng = None           # PhiloxStream; SMCsampler installs its own
+        self.debug_flags = 0      # SMCDET_MH_ABLATE_* timing diagnostics (never for sampling)
         self.last_loglik = None   # log-likelihood of the state returned by run()
 
     @staticmethod
@@ -107,7 +108,7 @@ class SingleComponentMH(object):
                               _hip.ptr(ru[2]).value)
         off = self.rng.take(self.num_iters)
         cm, cp, ch = image_model._cmodel(), prior._cprior(), self._cmh(prior)
-        flags = _hip.SMCDET_MH_FULL_RECOMPUTE if self.full_recompute else 0
+        flags = (_hip.SMCDET_MH_FULL_RECOMPUTE if self.full_recompute else 0) | self.debug_flags
         _hip.check(_hip.lib().smcdet_mh_sweep(
             _hip.ref(cm), _hip.ref(cp), _hip.ref(ch), _hip.ptr(data), _hip.ptr(temperature),
             T, N, S, anc_p, _hip.ptr(counts), _hip.ptr(locs), _hip.ptr(fluxes),
