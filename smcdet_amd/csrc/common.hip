@@ -64,6 +64,8 @@ DevModel make_dev_model(const smcdet_image_model_t& m) {
     d.kb = (float)(-beta / 2.0);
     d.p0 = (float)p0;
     d.inv_norm = (float)(1.0 / ((1.0 + b + p0) * (double)m.psf_norm));
+    d.lb2 = b > 0 ? (float)log2(b) : -INFINITY;
+    d.lp02 = p0 > 0 ? (float)log2(p0) : -INFINITY;
     d.s0sq = m.noise_additive;
     d.eta = m.noise_multiplicative;
   } else {

@@ -159,6 +159,7 @@ struct DevModel {
   float g;      // flux -> ADU scale (adu_per_nmgy; 1 for Poisson)
   // M71: psf(r2) = (exp2(k1 r2) + b exp2(k2 r2) + p0 exp2(kb log2(1 + k3 r2))) * inv_norm
   float k1, k2, b, k3, kb, p0, inv_norm;
+  float lb2, lp02;  // log2(b), log2(p0): b and p0 folded into the exponents
   // Poisson (basic) model: psf(r2) = amp * exp2(kg r2)
   float kg, amp;
   // M71 noise: var = s0sq + eta * rate
@@ -170,16 +171,25 @@ int validate_model(const smcdet_image_model_t* m);        // common.hip
 
 // M71ImageModel._compute_normalized_psf (images.py:137-145) / the basic
 // model's Normal(0, sigma).log_prob(r).exp() (images.py:17, 25-26)
+// psf_raw * psf_scale = the normalised profile
 template <int MODEL>
-__device__ __forceinline__ float psf_eval(const DevModel& m, float r2) {
+__device__ __forceinline__ float psf_raw(const DevModel& m, float r2) {
   if constexpr (MODEL == SMCDET_MODEL_M71) {
     const float t1 = fast_exp2(m.k1 * r2);
-    const float t2 = fast_exp2(m.k2 * r2);
-    const float t3 = fast_exp2(m.kb * fast_log2(fmaf(m.k3, r2, 1.0f)));
-    return (t1 + fmaf(m.b, t2, m.p0 * t3)) * m.inv_norm;
+    const float t2 = fast_exp2(fmaf(m.k2, r2, m.lb2));
+    const float t3 = fast_exp2(fmaf(m.kb, fast_log2(fmaf(m.k3, r2, 1.0f)), m.lp02));
+    return t1 + t2 + t3;
   } else {
-    return m.amp * fast_exp2(m.kg * r2);
+    return fast_exp2(m.kg * r2);
   }
+}
+template <int MODEL>
+__device__ __forceinline__ float psf_scale(const DevModel& m) {
+  return MODEL == SMCDET_MODEL_M71 ? m.inv_norm : m.amp;
+}
+template <int MODEL>
+__device__ __forceinline__ float psf_eval(const DevModel& m, float r2) {
+  return psf_raw<MODEL>(m, r2) * psf_scale<MODEL>(m);
 }
 
 // per-pixel log-likelihood: M71 Normal(rate, sqrt(s0^2 + eta*rate)).log_prob(x)
@@ -198,11 +208,10 @@ __device__ __forceinline__ float pix_loglik(const DevModel& m, float x, float lg
   }
 }
 
-// log(1 + a), accurate for small |a| (Goldberg's trick on the hardware log2)
+// log(1 + a), accurate for small |a|: log(u) - ((u - 1) - a)/u, u = fl(1 + a)
 __device__ __forceinline__ float log1p_fast(float a) {
   const float u = 1.0f + a;
-  if (u == 1.0f) return a;
-  return kLn2 * fast_log2(u) * (a * fast_rcp(u - 1.0f));
+  return fmaf(-((u - 1.0f) - a), fast_rcp(u), kLn2 * fast_log2(u));
 }
 
 // per-pixel log-likelihood CHANGE when the rate moves lam -> lam + dl, written
@@ -212,17 +221,25 @@ __device__ __forceinline__ float log1p_fast(float a) {
 template <int MODEL>
 __device__ __forceinline__ float pix_delta(const DevModel& m, float x, float lgx, float lam,
                                            float dl) {
-  const float lnew = lam + dl;
   if constexpr (MODEL == SMCDET_MODEL_M71) {
+    // v' = v (1 + a), a = eta dl / v;  d0^2/v - d1^2/v' = dl (eta d0^2/v + 2 d0 - dl) / (v (1+a))
     const float v0 = fmaf(m.eta, lam, m.s0sq);
-    const float v1 = fmaf(m.eta, lnew, m.s0sq);
+    const float r0 = fast_rcp(v0);
     const float d0 = x - lam;
-    const float num = dl * (fmaf(m.eta * d0, d0, 2.0f * d0 * v0) - dl * v0);
-    return 0.5f * num * fast_rcp(v0 * v1) - 0.5f * log1p_fast(m.eta * dl * fast_rcp(v0));
+    const float a = (m.eta * dl) * r0;
+    const float u = 1.0f + a;
+    const float ru = fast_rcp(u);
+    const float l1p = fmaf(-((u - 1.0f) - a), ru, kLn2 * fast_log2(u));  // log1p(a)
+    const float q = dl * fmaf(m.eta * d0, d0 * r0, fmaf(2.0f, d0, -dl)) * (r0 * ru);
+    return 0.5f * (q - l1p);
   } else {
+    const float lnew = lam + dl;
     if (lam > 50000.0f || lnew > 50000.0f)
       return pix_loglik<MODEL>(m, x, lgx, lnew) - pix_loglik<MODEL>(m, x, lgx, lam);
-    return x * log1p_fast(dl * fast_rcp(lam)) - dl;
+    const float a = dl * fast_rcp(lam);
+    const float u = 1.0f + a;
+    const float l1p = fmaf(-((u - 1.0f) - a), fast_rcp(u), kLn2 * fast_log2(u));
+    return fmaf(x, l1p, -dl);
   }
 }
 

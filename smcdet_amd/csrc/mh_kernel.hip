@@ -64,13 +64,96 @@ struct MhArgs {
   const float* r_uacc;
 };
 
-// truncated-normal cache at mean mu: Phi(lb), Z = Phi(ub) - Phi(lb), log Z
+// truncated-normal cache at mean mu: Phi(lb) and log Z, Z = Phi(ub) - Phi(lb)
 // (distributions.py:33-35)
 __device__ __forceinline__ void tn_cache(float mu, float isig, float lb, float ub, float& phl,
-                                         float& Z, float& lZ) {
+                                         float& lZ) {
   phl = normal_cdf(lb, mu, isig);
-  Z = normal_cdf(ub, mu, isig) - phl;
-  lZ = nan_to_num(fast_log(Z), 0.0f);
+  lZ = nan_to_num(fast_log(normal_cdf(ub, mu, isig) - phl), 0.0f);
+}
+
+// A proposal for one MH iteration: the chosen source j moves (h, w, f) ->
+// (hn, wn, fn).  Lanes 0,1,2 evaluate dimension h, w, flux in parallel; the
+// wave-uniform results are broadcast by v_readlane.  n_ph / n_lZ (per lane d)
+// are the truncated-normal caches at the proposed value, kept for the commit.
+struct Proposal {
+  int j;
+  float h, w, f, lf;      // current values of source j
+  float hn, wn, fn, lfn;  // proposed values
+  float hast;             // log q(z|z') - log q(z'|z)
+  float n_ph, n_lZ;       // per lane (d = lane < 3 ? lane : 2)
+};
+
+struct Dim {  // per-lane constants of the dimension this lane proposes
+  float sig, isig, lb, ub;
+};
+
+template <bool ABLATE>
+__device__ __forceinline__ Proposal propose(int j, float u, const Dim& dm, int d, float sh,
+                                            float sw, float sfx, float lfx, float ph_h, float lZ_h,
+                                            float ph_w, float lZ_w, float ph_f, float lZ_f) {
+  Proposal P;
+  P.j = j;
+  P.h = readlane(sh, j);
+  P.w = readlane(sw, j);
+  P.f = readlane(sfx, j);
+  P.lf = readlane(lfx, j);
+  const float c_ph = d == 0 ? readlane(ph_h, j) : (d == 1 ? readlane(ph_w, j) : readlane(ph_f, j));
+  const float c_lZ = d == 0 ? readlane(lZ_h, j) : (d == 1 ? readlane(lZ_w, j) : readlane(lZ_f, j));
+  const float mu = d == 0 ? P.h : (d == 1 ? P.w : P.f);
+  float xn, hast_d, n_lf;
+  if (ABLATE) {
+    xn = fminf(fmaxf(mu + (u - 0.5f) * dm.sig, dm.lb), dm.ub);
+    P.n_ph = c_ph;
+    P.n_lZ = c_lZ;
+    hast_d = 0.f;
+    n_lf = xn;
+  } else {
+    // TruncatedDiagonalMVN.sample (distributions.py:40-48)
+    const float pc = fminf(fmaxf(u, 1e-6f), 0.999999f);
+    float pt = c_ph + pc * fast_exp(c_lZ);
+    pt = fminf(fmaxf(pt, 1e-6f), 0.999999f);
+    xn = mu + dm.sig * erfinv_fast(2.0f * pt - 1.0f) * kSqrt2;
+    xn = fminf(fmaxf(xn, dm.lb), dm.ub);
+    tn_cache(xn, dm.isig, dm.lb, dm.ub, P.n_ph, P.n_lZ);
+    // the Normal log-densities cancel between numerator and denominator
+    // (kernel.py:71-111); the log-mass-in-box terms remain
+    hast_d = c_lZ - P.n_lZ;
+    n_lf = fast_log(xn);
+  }
+  P.hn = readlane(xn, 0);
+  P.wn = readlane(xn, 1);
+  P.fn = readlane(xn, 2);
+  P.hast = readlane(hast_d, 0) + readlane(hast_d, 1) + readlane(hast_d, 2);
+  P.lfn = readlane(n_lf, 2);
+  return P;
+}
+
+// One position of the union window: rate change dl and log-likelihood change.
+// WINDOWS = false when old and new windows coincide (same floor anchors): every
+// position of the (clipped) box is in both.
+template <int MODEL, bool WINDOWS>
+__device__ __forceinline__ float position_delta(const DevModel& m, const float* xs,
+                                                const float* lg, const float* lam, int p,
+                                                int aa, int bb, int ph, int pw,
+                                                const Proposal& P, float amp_o, float amp_n,
+                                                int ao_h, int ao_w, int an_h, int an_w,
+                                                float& lnew) {
+  const float fph = (float)ph + 0.5f, fpw = (float)pw + 0.5f;
+  const float dho = fph - P.h, dwo = fpw - P.w;
+  const float dhn = fph - P.hn, dwn = fpw - P.wn;
+  float psi_o = psf_raw<MODEL>(m, fmaf(dho, dho, dwo * dwo));
+  float psi_n = psf_raw<MODEL>(m, fmaf(dhn, dhn, dwn * dwn));
+  if (WINDOWS) {
+    const unsigned span = 2u * (unsigned)m.R;
+    psi_o = ((unsigned)(aa - ao_h) <= span && (unsigned)(bb - ao_w) <= span) ? psi_o : 0.f;
+    psi_n = ((unsigned)(aa - an_h) <= span && (unsigned)(bb - an_w) <= span) ? psi_n : 0.f;
+  }
+  const float dl = fmaf(amp_n, psi_n, -amp_o * psi_o);
+  const float lo = lam[p];
+  lnew = lo + dl;
+  const float lgx = (MODEL == SMCDET_MODEL_POISSON) ? lg[p] : 0.0f;
+  return pix_delta<MODEL>(m, xs[p], lgx, lo, dl);
 }
 
 template <int MODEL, bool REPLAY, bool FULL>
@@ -78,14 +161,19 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
   extern __shared__ float smem[];
   const DevModel& m = a.m;
   const int HW = m.H * m.W;
+  const int HWp = HW + 4;  // + a dummy cell (index HW) for masked lanes
   const int t = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   constexpr int kImg = (MODEL == SMCDET_MODEL_POISSON) ? 2 : 1;
   float* xs = smem;
-  float* lg = smem + HW;
-  float* lam = smem + kImg * HW + wave * HW;
+  float* lg = smem + HWp;
+  float* lam = smem + kImg * HWp + wave * HWp;
 
   stage_image<MODEL>(a.img + (size_t)t * HW, xs, lg, HW, threadIdx.x, kMhBlock);
+  if (threadIdx.x < 4) {
+    xs[HW + threadIdx.x] = m.bg;
+    if (MODEL == SMCDET_MODEL_POISSON) lg[HW + threadIdx.x] = 0.f;
+  }
   __syncthreads();
   const int n = blockIdx.x * kMhWaves + wave;
   if (n >= a.N) return;
@@ -104,226 +192,206 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
     sfx = a.fluxes_in[src * S + lane];
   }
   // per-source proposal caches at the current values
-  float ph_h, Z_h, lZ_h, ph_w, Z_w, lZ_w, ph_f, Z_f, lZ_f;
-  tn_cache(sh, a.isl, a.lb_h, a.ub_h, ph_h, Z_h, lZ_h);
-  tn_cache(sw, a.isl, a.lb_w, a.ub_w, ph_w, Z_w, lZ_w);
-  tn_cache(sfx, a.isf, a.lb_f, a.ub_f, ph_f, Z_f, lZ_f);
+  float ph_h, lZ_h, ph_w, lZ_w, ph_f, lZ_f;
+  tn_cache(sh, a.isl, a.lb_h, a.ub_h, ph_h, lZ_h);
+  tn_cache(sw, a.isl, a.lb_w, a.ub_w, ph_w, lZ_w);
+  tn_cache(sfx, a.isf, a.lb_f, a.ub_f, ph_f, lZ_f);
   float lfx = fast_log(sfx);
 
   const float tau = a.temperature[t];
   render_sources<MODEL>(m, lam, sh, sw, sfx, S, lane);
+  if (lane < 4) lam[HW + lane] = m.bg;
   double cur_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
 
   // lanes 0,1,2 handle proposal dimension d = h, w, flux
   const int d = lane < 3 ? lane : 2;
-  const float p_isig = d < 2 ? a.isl : a.isf;
-  const float p_sig = d < 2 ? a.sl : a.sf;
-  const float p_lb = d == 0 ? a.lb_h : (d == 1 ? a.lb_w : a.lb_f);
-  const float p_ub = d == 0 ? a.ub_h : (d == 1 ? a.ub_w : a.ub_f);
+  Dim dm;
+  dm.isig = d < 2 ? a.isl : a.isf;
+  dm.sig = d < 2 ? a.sl : a.sf;
+  dm.lb = d == 0 ? a.lb_h : (d == 1 ? a.lb_w : a.lb_f);
+  dm.ub = d == 0 ? a.ub_h : (d == 1 ? a.ub_w : a.ub_f);
+  const bool ablate_prop = (a.ablate & SMCDET_MH_ABLATE_PROPOSAL) != 0;
+  const bool ablate_lik = (a.ablate & SMCDET_MH_ABLATE_LIKELIHOOD) != 0;
 
+  // ---- draws: lane i of the cache holds iteration (block*64 + i) ------------
   float ru0 = 0.f, ru1 = 0.f, ru2 = 0.f, ru3 = 0.f, ru4 = 0.f;
   int rcomp = 0;
-  bool accept = false;
+  auto refill = [&](int k0) {
+    const int kk = k0 + lane;
+    if constexpr (REPLAY) {
+      if (kk < a.K) {
+        const size_t r = ((size_t)kk * a.T + t) * N + n;
+        rcomp = a.r_comp[r];
+        ru1 = a.r_uloc[r * 2 + 0];
+        ru2 = a.r_uloc[r * 2 + 1];
+        ru3 = a.r_uflux[r];
+        ru4 = a.r_uacc[r];
+      }
+    } else {
+      const uint64_t ctr = a.offset + (uint64_t)kk;
+      const uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32);
+      const U4 r0 = philox4x32(c0, c1, (uint32_t)pid, kTagMH0, a.k0, a.k1);
+      const U4 r1 = philox4x32(c0, c1, (uint32_t)pid, kTagMH1, a.k0, a.k1);
+      ru0 = u01(r0.x);
+      ru1 = u01(r0.y);
+      ru2 = u01(r0.z);
+      ru3 = u01(r0.w);
+      ru4 = u01(r1.x);
+    }
+  };
+  auto comp_of = [&](int kl) -> int {
+    if constexpr (REPLAY) return readlane(rcomp, kl);
+    else return min((int)(readlane(ru0, kl) * (float)S), S - 1);
+  };
+  auto uni_of = [&](int kl) -> float {
+    return d == 0 ? readlane(ru1, kl) : (d == 1 ? readlane(ru2, kl) : readlane(ru3, kl));
+  };
+  auto make_prop = [&](int kl) -> Proposal {
+    const int j = comp_of(kl);
+    const float u = uni_of(kl);
+    return ablate_prop ? propose<true>(j, u, dm, d, sh, sw, sfx, lfx, ph_h, lZ_h, ph_w, lZ_w,
+                                       ph_f, lZ_f)
+                       : propose<false>(j, u, dm, d, sh, sw, sfx, lfx, ph_h, lZ_h, ph_w, lZ_w,
+                                        ph_f, lZ_f);
+  };
 
+  int accept = 0;
+  Proposal P;
+  if (a.K > 0) {
+    refill(0);
+    P = make_prop(0);
+  }
   for (int k = 0; k < a.K; ++k) {
     const int kl = k & 63;
-    if (kl == 0) {
-      const int kk = k + lane;
-      if constexpr (REPLAY) {
-        if (kk < a.K) {
-          const size_t r = ((size_t)kk * a.T + t) * N + n;
-          rcomp = a.r_comp[r];
-          ru1 = a.r_uloc[r * 2 + 0];
-          ru2 = a.r_uloc[r * 2 + 1];
-          ru3 = a.r_uflux[r];
-          ru4 = a.r_uacc[r];
-        }
-      } else {
-        const uint64_t ctr = a.offset + (uint64_t)kk;
-        const uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32);
-        const U4 r0 = philox4x32(c0, c1, (uint32_t)pid, kTagMH0, a.k0, a.k1);
-        const U4 r1 = philox4x32(c0, c1, (uint32_t)pid, kTagMH1, a.k0, a.k1);
-        ru0 = u01(r0.x);
-        ru1 = u01(r0.y);
-        ru2 = u01(r0.z);
-        ru3 = u01(r0.w);
-        ru4 = u01(r1.x);
-      }
-    }
-    int j;
-    if constexpr (REPLAY) {
-      j = readlane(rcomp, kl);
-    } else {
-      j = min((int)(readlane(ru0, kl) * (float)S), S - 1);
-    }
     const float uacc = readlane(ru4, kl);
+    // software pipelining: the next iteration's proposal depends on this
+    // iteration only if both move the same source and this one is accepted,
+    // so it is computed now (overlapping the likelihood work) and redone in
+    // that rare case
+    if (kl == 63 && k + 1 < a.K) refill(k + 1);
+    Proposal Pn = P;
+    const bool has_next = k + 1 < a.K;
+    if (has_next) Pn = make_prop((k + 1) & 63);
 
-    // ---- current values and caches of source j -------------------------------
-    const float h = readlane(sh, j), w = readlane(sw, j), f = readlane(sfx, j);
-    const float lf = readlane(lfx, j);
-    const float c_ph = d == 0 ? readlane(ph_h, j) : (d == 1 ? readlane(ph_w, j) : readlane(ph_f, j));
-    const float c_lZ = d == 0 ? readlane(lZ_h, j) : (d == 1 ? readlane(lZ_w, j) : readlane(lZ_f, j));
-    const float mu = d == 0 ? h : (d == 1 ? w : f);
-    const float u = d == 0 ? readlane(ru1, kl) : (d == 1 ? readlane(ru2, kl) : readlane(ru3, kl));
-
-    // ---- truncated-normal proposal, lanes 0..2 (distributions.py:40-48) ------
-    float xn, n_ph, n_Z, n_lZ, hast_d, n_lf;
-    if (a.ablate & SMCDET_MH_ABLATE_PROPOSAL) {
-      // timing-only stand-in: a small deterministic move, no special functions
-      xn = fminf(fmaxf(mu + (u - 0.5f) * p_sig, p_lb), p_ub);
-      n_ph = c_ph;
-      n_Z = 1.f;
-      n_lZ = c_lZ;
-      hast_d = 0.f;
-      n_lf = xn;
-    } else {
-      const float pc = fminf(fmaxf(u, 1e-6f), 0.999999f);
-      float pt = c_ph + pc * fast_exp(c_lZ);
-      pt = fminf(fmaxf(pt, 1e-6f), 0.999999f);
-      xn = mu + p_sig * erfinv_fast(2.0f * pt - 1.0f) * kSqrt2;
-      xn = fminf(fmaxf(xn, p_lb), p_ub);
-      tn_cache(xn, p_isig, p_lb, p_ub, n_ph, n_Z, n_lZ);
-      hast_d = c_lZ - n_lZ;  // log q(z|z') - log q(z'|z), this dimension
-      n_lf = fast_log(xn);
-    }
-
-    const float hn = readlane(xn, 0), wn = readlane(xn, 1), fn = readlane(xn, 2);
-    const float hast = readlane(hast_d, 0) + readlane(hast_d, 1) + readlane(hast_d, 2);
-    const float lfn = readlane(n_lf, 2);
     // prior: uniform locations are constant in the box; flux density term
-    const float dprior = ((float)j < count) ? -a.pr.ap1 * (lfn - lf) : 0.0f;
+    const float dprior = ((float)P.j < count) ? -a.pr.ap1 * (P.lfn - P.lf) : 0.0f;
+    // rate contributions g*f*psf, the psf normalisation folded into the amplitude
+    const float amp_o = m.g * P.f * psf_scale<MODEL>(m), amp_n = m.g * P.fn * psf_scale<MODEL>(m);
 
     // ---- likelihood difference -----------------------------------------------
     float dll;
     double new_ll = 0.0;
-    const float amp_o = m.g * f, amp_n = m.g * fn;
-    // register slots for the incremental path
     float s_lam[kSlots];
     int s_pix[kSlots];
-    int r0 = 0, c0 = 0, bw = 1, npos = 0;
-    int fh0 = 0, fw0 = 0, fh1 = 0, fw1 = 0;
-    float inv_bw = 1.f;
+    int npos = 0, bw = 1, r0 = 0, c0 = 0;
+    unsigned magic = 65536u;
+    bool same = true;
+    int ao_h = 0, ao_w = 0, an_h = 0, an_w = 0;
     if constexpr (FULL) {
-      const float ch = lane == j ? hn : sh, cw = lane == j ? wn : sw, cf = lane == j ? fn : sfx;
+      const float ch = lane == P.j ? P.hn : sh, cw = lane == P.j ? P.wn : sw;
+      const float cf = lane == P.j ? P.fn : sfx;
       render_sources<MODEL>(m, lam, ch, cw, cf, S, lane);
       new_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
       dll = (float)(new_ll - cur_ll);
     } else {
-      fh0 = ifloor_clamped(h);
-      fw0 = ifloor_clamped(w);
-      fh1 = ifloor_clamped(hn);
-      fw1 = ifloor_clamped(wn);
+      const int fh0 = ifloor_clamped(P.h), fw0 = ifloor_clamped(P.w);
+      const int fh1 = ifloor_clamped(P.hn), fw1 = ifloor_clamped(P.wn);
       r0 = max(min(fh0, fh1) - m.R, 0);
       const int r1 = min(max(fh0, fh1) + m.R, m.H - 1);
       c0 = max(min(fw0, fw1) - m.R, 0);
       const int c1 = min(max(fw0, fw1) + m.R, m.W - 1);
       bw = c1 - c0 + 1;
-      npos = (r1 >= r0 && c1 >= c0 && !(a.ablate & SMCDET_MH_ABLATE_LIKELIHOOD))
-                 ? (r1 - r0 + 1) * bw : 0;
-      inv_bw = 1.0f / (float)bw;
+      npos = (r1 >= r0 && c1 >= c0 && !ablate_lik) ? (r1 - r0 + 1) * bw : 0;
+      magic = (65536u + (unsigned)bw - 1u) / (unsigned)bw;  // q / bw = (q*magic) >> 16, q < 1024
+      same = (fh0 == fh1) && (fw0 == fw1);
+      ao_h = fh0 - m.R - r0;
+      ao_w = fw0 - m.R - c0;
+      an_h = fh1 - m.R - r0;
+      an_w = fw1 - m.R - c0;
       float dsum = 0.f;
 #pragma unroll
       for (int i = 0; i < kSlots; ++i) {
-        s_pix[i] = -1;
+        s_pix[i] = HW;
+        s_lam[i] = 0.f;
         if (i * kWave < npos) {
           const int q = i * kWave + lane;
-          if (q < npos) {
-            const int aa = (int)(((float)q + 0.5f) * inv_bw);
-            const int bb = q - aa * bw;
-            const int ph = r0 + aa, pw = c0 + bb;
-            const int p = ph * m.W + pw;
-            const float fph = (float)ph + 0.5f, fpw = (float)pw + 0.5f;
-            float psi_o = 0.f, psi_n = 0.f;
-            if (abs(ph - fh0) <= m.R && abs(pw - fw0) <= m.R) {
-              const float dh = fph - h, dw = fpw - w;
-              psi_o = psf_eval<MODEL>(m, fmaf(dh, dh, dw * dw));
-            }
-            if (abs(ph - fh1) <= m.R && abs(pw - fw1) <= m.R) {
-              const float dh = fph - hn, dw = fpw - wn;
-              psi_n = psf_eval<MODEL>(m, fmaf(dh, dh, dw * dw));
-            }
-            const float dl = fmaf(amp_n, psi_n, -amp_o * psi_o);
-            const float lo = lam[p];
-            const float lgx = (MODEL == SMCDET_MODEL_POISSON) ? lg[p] : 0.0f;
-            dsum += pix_delta<MODEL>(m, xs[p], lgx, lo, dl);
-            s_lam[i] = lo + dl;
-            s_pix[i] = p;
-          }
+          const bool valid = q < npos;
+          const int aa = (int)(__umul24((unsigned)q, magic) >> 16);
+          const int bb = q - aa * bw;
+          const int ph = r0 + aa, pw = c0 + bb;
+          const int p = valid ? ph * m.W + pw : HW;
+          float lnew;
+          const float e =
+              same ? position_delta<MODEL, false>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
+                                                  amp_n, ao_h, ao_w, an_h, an_w, lnew)
+                   : position_delta<MODEL, true>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
+                                                 amp_n, ao_h, ao_w, an_h, an_w, lnew);
+          dsum += valid ? e : 0.f;
+          s_lam[i] = lnew;
+          s_pix[i] = p;
         }
       }
-      // rare: union window larger than the register slots (a jump of several px)
-      for (int q = kSlots * kWave + lane; q < npos; q += kWave) {
-        const int aa = (int)(((float)q + 0.5f) * inv_bw);
-        const int bb = q - aa * bw;
-        const int ph = r0 + aa, pw = c0 + bb;
-        const int p = ph * m.W + pw;
-        const float fph = (float)ph + 0.5f, fpw = (float)pw + 0.5f;
-        float psi_o = 0.f, psi_n = 0.f;
-        if (abs(ph - fh0) <= m.R && abs(pw - fw0) <= m.R) {
-          const float dh = fph - h, dw = fpw - w;
-          psi_o = psf_eval<MODEL>(m, fmaf(dh, dh, dw * dw));
+      // rare: a union window larger than the register slots (a jump of several px)
+      if (npos > kSlots * kWave) {
+        const float inv_bw = 1.0f / (float)bw;
+        for (int q = kSlots * kWave + lane; q < npos; q += kWave) {
+          const int aa = (int)(((float)q + 0.5f) * inv_bw);
+          const int bb = q - aa * bw;
+          const int ph = r0 + aa, pw = c0 + bb;
+          float lnew;
+          dsum += position_delta<MODEL, true>(m, xs, lg, lam, ph * m.W + pw, aa, bb, ph, pw, P,
+                                              amp_o, amp_n, ao_h, ao_w, an_h, an_w, lnew);
         }
-        if (abs(ph - fh1) <= m.R && abs(pw - fw1) <= m.R) {
-          const float dh = fph - hn, dw = fpw - wn;
-          psi_n = psf_eval<MODEL>(m, fmaf(dh, dh, dw * dw));
-        }
-        const float dl = fmaf(amp_n, psi_n, -amp_o * psi_o);
-        const float lgx = (MODEL == SMCDET_MODEL_POISSON) ? lg[p] : 0.0f;
-        dsum += pix_delta<MODEL>(m, xs[p], lgx, lam[p], dl);
       }
       dll = wave_sum(dsum);
     }
 
     // ---- accept / reject (kernel.py:114-128) ----------------------------------
-    const float loga = dprior + tau * dll + hast;
+    const float loga = dprior + tau * dll + P.hast;
     const float e = fast_exp(loga);
     const float alpha = e > 1.0f ? 1.0f : e;  // clamp(max=1) keeps NaN
-    accept = uacc <= alpha;
+    accept = __builtin_amdgcn_readfirstlane((uacc <= alpha) ? 1 : 0);
     if (accept) {
       if constexpr (FULL) {
         cur_ll = new_ll;
       } else {
 #pragma unroll
-        for (int i = 0; i < kSlots; ++i) {
-          if (i * kWave < npos && s_pix[i] >= 0) {
-            lam[s_pix[i]] = s_lam[i];
+        for (int i = 0; i < kSlots; ++i)
+          if (i * kWave < npos) lam[s_pix[i]] = s_lam[i];
+        if (npos > kSlots * kWave) {
+          const float inv_bw = 1.0f / (float)bw;
+          for (int q = kSlots * kWave + lane; q < npos; q += kWave) {
+            const int aa = (int)(((float)q + 0.5f) * inv_bw);
+            const int bb = q - aa * bw;
+            const int ph = r0 + aa, pw = c0 + bb;
+            float lnew;
+            (void)position_delta<MODEL, true>(m, xs, lg, lam, ph * m.W + pw, aa, bb, ph, pw, P,
+                                              amp_o, amp_n, ao_h, ao_w, an_h, an_w, lnew);
+            lam[ph * m.W + pw] = lnew;
           }
-        }
-        for (int q = kSlots * kWave + lane; q < npos; q += kWave) {
-          const int aa = (int)(((float)q + 0.5f) * inv_bw);
-          const int bb = q - aa * bw;
-          const int ph = r0 + aa, pw = c0 + bb;
-          const int p = ph * m.W + pw;
-          const float fph = (float)ph + 0.5f, fpw = (float)pw + 0.5f;
-          float psi_o = 0.f, psi_n = 0.f;
-          if (abs(ph - fh0) <= m.R && abs(pw - fw0) <= m.R) {
-            const float dh = fph - h, dw = fpw - w;
-            psi_o = psf_eval<MODEL>(m, fmaf(dh, dh, dw * dw));
-          }
-          if (abs(ph - fh1) <= m.R && abs(pw - fw1) <= m.R) {
-            const float dh = fph - hn, dw = fpw - wn;
-            psi_n = psf_eval<MODEL>(m, fmaf(dh, dh, dw * dw));
-          }
-          lam[p] += fmaf(amp_n, psi_n, -amp_o * psi_o);
         }
         cur_ll += (double)dll;
         wave_sync();
       }
-      const float nph_h = readlane(n_ph, 0), nZ_h = readlane(n_Z, 0), nlZ_h = readlane(n_lZ, 0);
-      const float nph_w = readlane(n_ph, 1), nZ_w = readlane(n_Z, 1), nlZ_w = readlane(n_lZ, 1);
-      const float nph_f = readlane(n_ph, 2), nZ_f = readlane(n_Z, 2), nlZ_f = readlane(n_lZ, 2);
-      if (lane == j) {
-        sh = hn;
-        sw = wn;
-        sfx = fn;
-        lfx = lfn;
-        ph_h = nph_h; Z_h = nZ_h; lZ_h = nlZ_h;
-        ph_w = nph_w; Z_w = nZ_w; lZ_w = nlZ_w;
-        ph_f = nph_f; Z_f = nZ_f; lZ_f = nlZ_f;
-      }
+      const bool me = lane == P.j;
+      sh = me ? P.hn : sh;
+      sw = me ? P.wn : sw;
+      sfx = me ? P.fn : sfx;
+      lfx = me ? P.lfn : lfx;
+      const float nph_h = readlane(P.n_ph, 0), nlZ_h = readlane(P.n_lZ, 0);
+      const float nph_w = readlane(P.n_ph, 1), nlZ_w = readlane(P.n_lZ, 1);
+      const float nph_f = readlane(P.n_ph, 2), nlZ_f = readlane(P.n_lZ, 2);
+      ph_h = me ? nph_h : ph_h;
+      lZ_h = me ? nlZ_h : lZ_h;
+      ph_w = me ? nph_w : ph_w;
+      lZ_w = me ? nlZ_w : lZ_w;
+      ph_f = me ? nph_f : ph_f;
+      lZ_f = me ? nlZ_f : lZ_f;
+      // the speculative next proposal read source P.j's old state: redo it
+      if (has_next && Pn.j == P.j) Pn = make_prop((k + 1) & 63);
     }
+    P = Pn;
   }
-  (void)Z_h; (void)Z_w; (void)Z_f;
 
   // ---- write back --------------------------------------------------------------
   if (lane < S) {
@@ -436,9 +504,9 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(acc_count, 0, (size_t)T * sizeof(int32_t), st) != hipSuccess)
     return set_error(SMCDET_EHIP, "smcdet_mh_sweep: memset failed");
-  const size_t HW = (size_t)model->H * model->W;
+  const size_t HWp = (size_t)model->H * model->W + 4;
   const size_t lds =
-      ((model->model == SMCDET_MODEL_POISSON ? 2 : 1) * HW + (size_t)kMhWaves * HW) *
+      ((model->model == SMCDET_MODEL_POISSON ? 2 : 1) * HWp + (size_t)kMhWaves * HWp) *
       sizeof(float);
   const dim3 grid((N + kMhWaves - 1) / kMhWaves, T);
   const bool full = (flags & SMCDET_MH_FULL_RECOMPUTE) != 0;
