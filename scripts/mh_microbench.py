@@ -52,11 +52,14 @@ def main():
                 "no_both": (False, 768)}
     if a.full:
         variants["full_recompute"] = (True, 0)
+    for kk in (0, 1, 25, 200):
+        variants[f"K={kk}"] = (False, 0, kk)
     times = {k: [] for k in variants}
     times["tile_kernel"] = []
     mhs = {}
-    for k, (full, fl) in variants.items():
-        mh = p_m71_mh(a.K, full_recompute=full)
+    for k, v in variants.items():
+        full, fl = v[0], v[1]
+        mh = p_m71_mh(v[2] if len(v) > 2 else a.K, full_recompute=full)
         mh.debug_flags = fl
         mhs[k] = mh
     ll = model.loglikelihood(img, locs, fluxes)
@@ -84,11 +87,30 @@ def main():
         torch.cuda.synchronize()
         if r:
             times["tile_kernel"].append(e0.elapsed_time(e1))
+        # its three parts separately
+        parts = {
+            "temper_only": lambda: _hip.lib().smcdet_temper(
+                _hip.ptr(ll), _hip.ptr(torch.zeros(T, device=dev)), _hip.ptr(tp), T, Np,
+                0.5 * Np, _hip.stream_of(ll)),
+            "weights_only": lambda: _hip.lib().smcdet_update_weights(
+                _hip.ptr(ll), _hip.ptr(t_), _hip.ptr(tp), _hip.ptr(lw), _hip.ptr(W),
+                _hip.ptr(ess), _hip.ptr(lz), T, Np, _hip.stream_of(ll)),
+            "resample_only": lambda: _hip.lib().smcdet_resample_index(
+                _hip.ptr(W), T, Np, 1, 1, 0, None, _hip.ptr(idx), _hip.stream_of(ll)),
+        }
+        for name, fn in parts.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _hip.check(fn(), name)
+            e1.record()
+            torch.cuda.synchronize()
+            if r:
+                times.setdefault(name, []).append(e0.elapsed_time(e1))
     out = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))}
            for k, v in times.items()}
     steps = nt * nt * Np * a.K
     for k, v in out.items():
-        if k != "tile_kernel":
+        if k in variants and not k.startswith("K="):
             v["particle_steps_per_s"] = steps / (v["median_ms"] * 1e-3)
     print(json.dumps({"config": vars(a), "variants": out}, indent=1))
 

@@ -29,6 +29,8 @@
 // returned loglik_out comes from a fresh full render of the final state.
 #include <math.h>
 
+#include <type_traits>
+
 #include "render.h"
 
 namespace smcdet {
@@ -98,8 +100,11 @@ __device__ __forceinline__ Proposal propose(int j, float u, const Dim& dm, int d
   P.w = readlane(sw, j);
   P.f = readlane(sfx, j);
   P.lf = readlane(lfx, j);
-  const float c_ph = d == 0 ? readlane(ph_h, j) : (d == 1 ? readlane(ph_w, j) : readlane(ph_f, j));
-  const float c_lZ = d == 0 ? readlane(lZ_h, j) : (d == 1 ? readlane(lZ_w, j) : readlane(lZ_f, j));
+  // v_readlane is convergent: read all three unconditionally, then select per lane
+  const float ph0 = readlane(ph_h, j), ph1 = readlane(ph_w, j), ph2 = readlane(ph_f, j);
+  const float lz0 = readlane(lZ_h, j), lz1 = readlane(lZ_w, j), lz2 = readlane(lZ_f, j);
+  const float c_ph = d == 0 ? ph0 : (d == 1 ? ph1 : ph2);
+  const float c_lZ = d == 0 ? lz0 : (d == 1 ? lz1 : lz2);
   const float mu = d == 0 ? P.h : (d == 1 ? P.w : P.f);
   float xn, hast_d, n_lf;
   if (ABLATE) {
@@ -161,7 +166,7 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
   extern __shared__ float smem[];
   const DevModel& m = a.m;
   const int HW = m.H * m.W;
-  const int HWp = HW + 4;  // + a dummy cell (index HW) for masked lanes
+  const int HWp = HW + kWave;  // + one dummy cell per lane (HW + lane) for masked lanes
   const int t = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   constexpr int kImg = (MODEL == SMCDET_MODEL_POISSON) ? 2 : 1;
@@ -170,7 +175,7 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
   float* lam = smem + kImg * HWp + wave * HWp;
 
   stage_image<MODEL>(a.img + (size_t)t * HW, xs, lg, HW, threadIdx.x, kMhBlock);
-  if (threadIdx.x < 4) {
+  if (threadIdx.x < kWave) {
     xs[HW + threadIdx.x] = m.bg;
     if (MODEL == SMCDET_MODEL_POISSON) lg[HW + threadIdx.x] = 0.f;
   }
@@ -200,7 +205,7 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
 
   const float tau = a.temperature[t];
   render_sources<MODEL>(m, lam, sh, sw, sfx, S, lane);
-  if (lane < 4) lam[HW + lane] = m.bg;
+  lam[HW + lane] = m.bg;
   double cur_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
 
   // lanes 0,1,2 handle proposal dimension d = h, w, flux
@@ -241,10 +246,11 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
   };
   auto comp_of = [&](int kl) -> int {
     if constexpr (REPLAY) return readlane(rcomp, kl);
-    else return min((int)(readlane(ru0, kl) * (float)S), S - 1);
+    else return __builtin_amdgcn_readfirstlane(min((int)(readlane(ru0, kl) * (float)S), S - 1));
   };
   auto uni_of = [&](int kl) -> float {
-    return d == 0 ? readlane(ru1, kl) : (d == 1 ? readlane(ru2, kl) : readlane(ru3, kl));
+    const float u1 = readlane(ru1, kl), u2 = readlane(ru2, kl), u3 = readlane(ru3, kl);
+    return d == 0 ? u1 : (d == 1 ? u2 : u3);
   };
   auto make_prop = [&](int kl) -> Proposal {
     const int j = comp_of(kl);
@@ -269,9 +275,9 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
     // so it is computed now (overlapping the likelihood work) and redone in
     // that rare case
     if (kl == 63 && k + 1 < a.K) refill(k + 1);
-    Proposal Pn = P;
     const bool has_next = k + 1 < a.K;
-    if (has_next) Pn = make_prop((k + 1) & 63);
+    const int kn = (k + 1) & 63;
+    Proposal Pn = P;
 
     // prior: uniform locations are constant in the box; flux density term
     const float dprior = ((float)P.j < count) ? -a.pr.ap1 * (P.lfn - P.lf) : 0.0f;
@@ -283,11 +289,9 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
     double new_ll = 0.0;
     float s_lam[kSlots];
     int s_pix[kSlots];
-    int npos = 0, bw = 1, r0 = 0, c0 = 0;
-    unsigned magic = 65536u;
-    bool same = true;
-    int ao_h = 0, ao_w = 0, an_h = 0, an_w = 0;
+    int npos = 0, bw = 1, r0 = 0, c0 = 0, nslots = 0;
     if constexpr (FULL) {
+      if (has_next) Pn = make_prop(kn);
       const float ch = lane == P.j ? P.hn : sh, cw = lane == P.j ? P.wn : sw;
       const float cf = lane == P.j ? P.fn : sfx;
       render_sources<MODEL>(m, lam, ch, cw, cf, S, lane);
@@ -302,45 +306,65 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
       const int c1 = min(max(fw0, fw1) + m.R, m.W - 1);
       bw = c1 - c0 + 1;
       npos = (r1 >= r0 && c1 >= c0 && !ablate_lik) ? (r1 - r0 + 1) * bw : 0;
-      magic = (65536u + (unsigned)bw - 1u) / (unsigned)bw;  // q / bw = (q*magic) >> 16, q < 1024
-      same = (fh0 == fh1) && (fw0 == fw1);
-      ao_h = fh0 - m.R - r0;
-      ao_w = fw0 - m.R - c0;
-      an_h = fh1 - m.R - r0;
-      an_w = fw1 - m.R - c0;
-      float dsum = 0.f;
+      nslots = (npos + kWave - 1) / kWave;
+      const unsigned magic = (65536u + (unsigned)bw - 1u) / (unsigned)bw;  // q/bw, q < 1024
+      const bool same = (fh0 == fh1) && (fw0 == fw1);
+      const int ao_h = fh0 - m.R - r0, ao_w = fw0 - m.R - c0;
+      const int an_h = fh1 - m.R - r0, an_w = fw1 - m.R - c0;
 #pragma unroll
       for (int i = 0; i < kSlots; ++i) {
-        s_pix[i] = HW;
+        s_pix[i] = HW + lane;
         s_lam[i] = 0.f;
-        if (i * kWave < npos) {
+      }
+      // NS predicated slots in one basic block, with the (independent) next
+      // proposal in the same block so the scheduler can interleave the two
+      auto slots = [&](auto NS, auto WIN) -> float {
+        constexpr int ns = decltype(NS)::value;
+        constexpr bool win = decltype(WIN)::value;
+        if (has_next) Pn = make_prop(kn);
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < ns; ++i) {
           const int q = i * kWave + lane;
           const bool valid = q < npos;
           const int aa = (int)(__umul24((unsigned)q, magic) >> 16);
           const int bb = q - aa * bw;
           const int ph = r0 + aa, pw = c0 + bb;
-          const int p = valid ? ph * m.W + pw : HW;
+          const int p = valid ? ph * m.W + pw : HW + lane;
           float lnew;
-          const float e =
-              same ? position_delta<MODEL, false>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
-                                                  amp_n, ao_h, ao_w, an_h, an_w, lnew)
-                   : position_delta<MODEL, true>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
-                                                 amp_n, ao_h, ao_w, an_h, an_w, lnew);
-          dsum += valid ? e : 0.f;
+          const float e = position_delta<MODEL, win>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
+                                                     amp_n, ao_h, ao_w, an_h, an_w, lnew);
+          acc += valid ? e : 0.f;
           s_lam[i] = lnew;
           s_pix[i] = p;
         }
-      }
-      // rare: a union window larger than the register slots (a jump of several px)
-      if (npos > kSlots * kWave) {
-        const float inv_bw = 1.0f / (float)bw;
-        for (int q = kSlots * kWave + lane; q < npos; q += kWave) {
-          const int aa = (int)(((float)q + 0.5f) * inv_bw);
-          const int bb = q - aa * bw;
-          const int ph = r0 + aa, pw = c0 + bb;
-          float lnew;
-          dsum += position_delta<MODEL, true>(m, xs, lg, lam, ph * m.W + pw, aa, bb, ph, pw, P,
-                                              amp_o, amp_n, ao_h, ao_w, an_h, an_w, lnew);
+        return acc;
+      };
+      using I3 = std::integral_constant<int, 3>;
+      using I5 = std::integral_constant<int, 5>;
+      using I8 = std::integral_constant<int, kSlots>;
+      using Win = std::true_type;
+      using Same = std::false_type;
+      float dsum = 0.f;
+      if (nslots == 0) {
+        if (has_next) Pn = make_prop(kn);
+      } else if (nslots <= 3) {
+        dsum = same ? slots(I3{}, Same{}) : slots(I3{}, Win{});
+      } else if (nslots <= 5) {
+        dsum = same ? slots(I5{}, Same{}) : slots(I5{}, Win{});
+      } else {
+        dsum = slots(I8{}, Win{});
+        // rare: a union window larger than the register slots (a jump of several px)
+        if (npos > kSlots * kWave) {
+          const float inv_bw = 1.0f / (float)bw;
+          for (int q = kSlots * kWave + lane; q < npos; q += kWave) {
+            const int aa = (int)(((float)q + 0.5f) * inv_bw);
+            const int bb = q - aa * bw;
+            const int ph = r0 + aa, pw = c0 + bb;
+            float lnew;
+            dsum += position_delta<MODEL, true>(m, xs, lg, lam, ph * m.W + pw, aa, bb, ph, pw,
+                                                P, amp_o, amp_n, ao_h, ao_w, an_h, an_w, lnew);
+          }
         }
       }
       dll = wave_sum(dsum);
@@ -357,8 +381,12 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
       } else {
 #pragma unroll
         for (int i = 0; i < kSlots; ++i)
-          if (i * kWave < npos) lam[s_pix[i]] = s_lam[i];
+          if (i < nslots) lam[s_pix[i]] = s_lam[i];
         if (npos > kSlots * kWave) {
+          const int fh0 = ifloor_clamped(P.h), fw0 = ifloor_clamped(P.w);
+          const int fh1 = ifloor_clamped(P.hn), fw1 = ifloor_clamped(P.wn);
+          const int ao_h = fh0 - m.R - r0, ao_w = fw0 - m.R - c0;
+          const int an_h = fh1 - m.R - r0, an_w = fw1 - m.R - c0;
           const float inv_bw = 1.0f / (float)bw;
           for (int q = kSlots * kWave + lane; q < npos; q += kWave) {
             const int aa = (int)(((float)q + 0.5f) * inv_bw);
@@ -504,7 +532,7 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(acc_count, 0, (size_t)T * sizeof(int32_t), st) != hipSuccess)
     return set_error(SMCDET_EHIP, "smcdet_mh_sweep: memset failed");
-  const size_t HWp = (size_t)model->H * model->W + 4;
+  const size_t HWp = (size_t)model->H * model->W + kWave;
   const size_t lds =
       ((model->model == SMCDET_MODEL_POISSON ? 2 : 1) * HWp + (size_t)kMhWaves * HWp) *
       sizeof(float);
