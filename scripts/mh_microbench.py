@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--K", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--full", action="store_true", help="include the full-recompute variant")
+    ap.add_argument("--only", default=None, help="run just this variant (for rocprofv3 --pmc)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -54,6 +55,8 @@ def main():
         variants["full_recompute"] = (True, 0)
     for kk in (0, 1, 25, 200):
         variants[f"K={kk}"] = (False, 0, kk)
+    if a.only:
+        variants = {a.only: variants[a.only]}
     times = {k: [] for k in variants}
     times["tile_kernel"] = []
     mhs = {}

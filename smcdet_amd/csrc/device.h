@@ -286,7 +286,7 @@ __device__ __forceinline__ float erfinv_fast(float x) {
   pa = fmaf(pa, wa, -0.00417768164f);
   pa = fmaf(pa, wa, 0.246640727f);
   pa = fmaf(pa, wa, 1.50140941f);
-  const float wb = sqrtf(w) - 3.0f;
+  const float wb = __builtin_amdgcn_sqrtf(w) - 3.0f;
   float pb = -0.000200214257f;
   pb = fmaf(pb, wb, 0.000100950558f);
   pb = fmaf(pb, wb, 0.00134934322f);

@@ -37,7 +37,8 @@ namespace smcdet {
 
 constexpr int kMhWaves = 4;
 constexpr int kMhBlock = kMhWaves * kWave;
-constexpr int kSlots = 8;  // register-resident window passes (8*64 = 512 positions)
+constexpr int kSlots = 6;  // register-resident window passes (6*64 = 384 positions)
+constexpr int kBatch = 8;  // proposals computed together (3 lanes each)
 
 struct MhArgs {
   DevModel m;
@@ -75,63 +76,43 @@ __device__ __forceinline__ void tn_cache(float mu, float isig, float lb, float u
 }
 
 // A proposal for one MH iteration: the chosen source j moves (h, w, f) ->
-// (hn, wn, fn).  Lanes 0,1,2 evaluate dimension h, w, flux in parallel; the
-// wave-uniform results are broadcast by v_readlane.  n_ph / n_lZ (per lane d)
-// are the truncated-normal caches at the proposed value, kept for the commit.
+// (hn, wn, fn).  Wave-uniform (SGPR) values.
 struct Proposal {
   int j;
   float h, w, f, lf;      // current values of source j
   float hn, wn, fn, lfn;  // proposed values
   float hast;             // log q(z|z') - log q(z'|z)
-  float n_ph, n_lZ;       // per lane (d = lane < 3 ? lane : 2)
 };
 
 struct Dim {  // per-lane constants of the dimension this lane proposes
   float sig, isig, lb, ub;
 };
 
+// One dimension of one truncated-normal proposal (distributions.py:40-48),
+// evaluated by one lane: mu = current value, (c_ph, c_lZ) its cached Phi(lb)
+// and log-mass-in-box; returns the proposed value, the caches at it, the
+// dimension's Hastings term and log(value).  The Normal log-densities of
+// q(z|z') and q(z'|z) cancel (kernel.py:71-111); the log-mass terms remain.
 template <bool ABLATE>
-__device__ __forceinline__ Proposal propose(int j, float u, const Dim& dm, int d, float sh,
-                                            float sw, float sfx, float lfx, float ph_h, float lZ_h,
-                                            float ph_w, float lZ_w, float ph_f, float lZ_f) {
-  Proposal P;
-  P.j = j;
-  P.h = readlane(sh, j);
-  P.w = readlane(sw, j);
-  P.f = readlane(sfx, j);
-  P.lf = readlane(lfx, j);
-  // v_readlane is convergent: read all three unconditionally, then select per lane
-  const float ph0 = readlane(ph_h, j), ph1 = readlane(ph_w, j), ph2 = readlane(ph_f, j);
-  const float lz0 = readlane(lZ_h, j), lz1 = readlane(lZ_w, j), lz2 = readlane(lZ_f, j);
-  const float c_ph = d == 0 ? ph0 : (d == 1 ? ph1 : ph2);
-  const float c_lZ = d == 0 ? lz0 : (d == 1 ? lz1 : lz2);
-  const float mu = d == 0 ? P.h : (d == 1 ? P.w : P.f);
-  float xn, hast_d, n_lf;
-  if (ABLATE) {
+__device__ __forceinline__ void propose_lane(float mu, float c_ph, float c_lZ, float u,
+                                             const Dim& dm, float& xn, float& n_ph, float& n_lZ,
+                                             float& hast_d, float& n_lf) {
+  if (ABLATE) {  // timing-only stand-in: a small deterministic move
     xn = fminf(fmaxf(mu + (u - 0.5f) * dm.sig, dm.lb), dm.ub);
-    P.n_ph = c_ph;
-    P.n_lZ = c_lZ;
+    n_ph = c_ph;
+    n_lZ = c_lZ;
     hast_d = 0.f;
     n_lf = xn;
   } else {
-    // TruncatedDiagonalMVN.sample (distributions.py:40-48)
     const float pc = fminf(fmaxf(u, 1e-6f), 0.999999f);
     float pt = c_ph + pc * fast_exp(c_lZ);
     pt = fminf(fmaxf(pt, 1e-6f), 0.999999f);
     xn = mu + dm.sig * erfinv_fast(2.0f * pt - 1.0f) * kSqrt2;
     xn = fminf(fmaxf(xn, dm.lb), dm.ub);
-    tn_cache(xn, dm.isig, dm.lb, dm.ub, P.n_ph, P.n_lZ);
-    // the Normal log-densities cancel between numerator and denominator
-    // (kernel.py:71-111); the log-mass-in-box terms remain
-    hast_d = c_lZ - P.n_lZ;
+    tn_cache(xn, dm.isig, dm.lb, dm.ub, n_ph, n_lZ);
+    hast_d = c_lZ - n_lZ;
     n_lf = fast_log(xn);
   }
-  P.hn = readlane(xn, 0);
-  P.wn = readlane(xn, 1);
-  P.fn = readlane(xn, 2);
-  P.hast = readlane(hast_d, 0) + readlane(hast_d, 1) + readlane(hast_d, 2);
-  P.lfn = readlane(n_lf, 2);
-  return P;
 }
 
 // One position of the union window: rate change dl and log-likelihood change.
@@ -162,7 +143,7 @@ __device__ __forceinline__ float position_delta(const DevModel& m, const float* 
 }
 
 template <int MODEL, bool REPLAY, bool FULL>
-__global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
+__global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   extern __shared__ float smem[];
   const DevModel& m = a.m;
   const int HW = m.H * m.W;
@@ -208,8 +189,12 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
   lam[HW + lane] = m.bg;
   double cur_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
 
-  // lanes 0,1,2 handle proposal dimension d = h, w, flux
-  const int d = lane < 3 ? lane : 2;
+  // ---- proposals, batched: lane 3b+d proposes dimension d (h, w, flux) of
+  // iteration batch_k0 + b (b < kBatch), from the state at batch time.  An
+  // entry goes stale only if an earlier accepted iteration of the batch moved
+  // the same source (tracked in `dirty`); the batch is then recomputed.
+  const int lb3 = lane / 3;
+  const int d = lane - 3 * lb3;
   Dim dm;
   dm.isig = d < 2 ? a.isl : a.isf;
   dm.sig = d < 2 ? a.sl : a.sf;
@@ -244,40 +229,62 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
       ru4 = u01(r1.x);
     }
   };
-  auto comp_of = [&](int kl) -> int {
-    if constexpr (REPLAY) return readlane(rcomp, kl);
-    else return __builtin_amdgcn_readfirstlane(min((int)(readlane(ru0, kl) * (float)S), S - 1));
-  };
-  auto uni_of = [&](int kl) -> float {
-    const float u1 = readlane(ru1, kl), u2 = readlane(ru2, kl), u3 = readlane(ru3, kl);
-    return d == 0 ? u1 : (d == 1 ? u2 : u3);
-  };
-  auto make_prop = [&](int kl) -> Proposal {
-    const int j = comp_of(kl);
-    const float u = uni_of(kl);
-    return ablate_prop ? propose<true>(j, u, dm, d, sh, sw, sfx, lfx, ph_h, lZ_h, ph_w, lZ_w,
-                                       ph_f, lZ_f)
-                       : propose<false>(j, u, dm, d, sh, sw, sfx, lfx, ph_h, lZ_h, ph_w, lZ_w,
-                                        ph_f, lZ_f);
+
+  float bx = 0.f, bph = 0.f, blZ = 0.f, bhd = 0.f, blf = 0.f;
+  int bj = 0, batch_k0 = 0, batch_n = 0;
+  uint64_t dirty = 0;
+  auto compute_batch = [&](int k0) {
+    const int n_ = min(min(kBatch, kWave - (k0 & 63)), a.K - k0);
+    const int b = min(lb3, n_ - 1);
+    const int kl = (k0 & 63) + b;
+    int j;
+    if constexpr (REPLAY) j = __shfl(rcomp, kl, kWave);
+    else j = min((int)(__shfl(ru0, kl, kWave) * (float)S), S - 1);
+    const float u1 = __shfl(ru1, kl, kWave), u2 = __shfl(ru2, kl, kWave);
+    const float u3 = __shfl(ru3, kl, kWave);
+    const float u = d == 0 ? u1 : (d == 1 ? u2 : u3);
+    const float m0 = __shfl(sh, j, kWave), m1 = __shfl(sw, j, kWave), m2 = __shfl(sfx, j, kWave);
+    const float q0 = __shfl(ph_h, j, kWave), q1 = __shfl(ph_w, j, kWave);
+    const float q2 = __shfl(ph_f, j, kWave);
+    const float z0 = __shfl(lZ_h, j, kWave), z1 = __shfl(lZ_w, j, kWave);
+    const float z2 = __shfl(lZ_f, j, kWave);
+    const float mu = d == 0 ? m0 : (d == 1 ? m1 : m2);
+    const float c_ph = d == 0 ? q0 : (d == 1 ? q1 : q2);
+    const float c_lZ = d == 0 ? z0 : (d == 1 ? z1 : z2);
+    if (ablate_prop)
+      propose_lane<true>(mu, c_ph, c_lZ, u, dm, bx, bph, blZ, bhd, blf);
+    else
+      propose_lane<false>(mu, c_ph, c_lZ, u, dm, bx, bph, blZ, bhd, blf);
+    bj = j;
+    batch_k0 = k0;
+    batch_n = n_;
+    dirty = 0;
   };
 
   int accept = 0;
-  Proposal P;
-  if (a.K > 0) {
-    refill(0);
-    P = make_prop(0);
-  }
   for (int k = 0; k < a.K; ++k) {
     const int kl = k & 63;
+    if (kl == 0) refill(k);
+    if (k >= batch_k0 + batch_n) compute_batch(k);
+    int b = k - batch_k0;
+    int j = readlane(bj, 3 * b);
+    if ((dirty >> j) & 1ull) {
+      compute_batch(k);
+      b = 0;
+      j = readlane(bj, 0);
+    }
     const float uacc = readlane(ru4, kl);
-    // software pipelining: the next iteration's proposal depends on this
-    // iteration only if both move the same source and this one is accepted,
-    // so it is computed now (overlapping the likelihood work) and redone in
-    // that rare case
-    if (kl == 63 && k + 1 < a.K) refill(k + 1);
-    const bool has_next = k + 1 < a.K;
-    const int kn = (k + 1) & 63;
-    Proposal Pn = P;
+    Proposal P;
+    P.j = j;
+    P.h = readlane(sh, j);
+    P.w = readlane(sw, j);
+    P.f = readlane(sfx, j);
+    P.lf = readlane(lfx, j);
+    P.hn = readlane(bx, 3 * b);
+    P.wn = readlane(bx, 3 * b + 1);
+    P.fn = readlane(bx, 3 * b + 2);
+    P.hast = readlane(bhd, 3 * b) + readlane(bhd, 3 * b + 1) + readlane(bhd, 3 * b + 2);
+    P.lfn = readlane(blf, 3 * b + 2);
 
     // prior: uniform locations are constant in the box; flux density term
     const float dprior = ((float)P.j < count) ? -a.pr.ap1 * (P.lfn - P.lf) : 0.0f;
@@ -291,7 +298,6 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
     int s_pix[kSlots];
     int npos = 0, bw = 1, r0 = 0, c0 = 0, nslots = 0;
     if constexpr (FULL) {
-      if (has_next) Pn = make_prop(kn);
       const float ch = lane == P.j ? P.hn : sh, cw = lane == P.j ? P.wn : sw;
       const float cf = lane == P.j ? P.fn : sfx;
       render_sources<MODEL>(m, lam, ch, cw, cf, S, lane);
@@ -311,17 +317,11 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
       const bool same = (fh0 == fh1) && (fw0 == fw1);
       const int ao_h = fh0 - m.R - r0, ao_w = fw0 - m.R - c0;
       const int an_h = fh1 - m.R - r0, an_w = fw1 - m.R - c0;
-#pragma unroll
-      for (int i = 0; i < kSlots; ++i) {
-        s_pix[i] = HW + lane;
-        s_lam[i] = 0.f;
-      }
       // NS predicated slots in one basic block, with the (independent) next
       // proposal in the same block so the scheduler can interleave the two
       auto slots = [&](auto NS, auto WIN) -> float {
         constexpr int ns = decltype(NS)::value;
         constexpr bool win = decltype(WIN)::value;
-        if (has_next) Pn = make_prop(kn);
         float acc = 0.f;
 #pragma unroll
         for (int i = 0; i < ns; ++i) {
@@ -347,7 +347,6 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
       using Same = std::false_type;
       float dsum = 0.f;
       if (nslots == 0) {
-        if (has_next) Pn = make_prop(kn);
       } else if (nslots <= 3) {
         dsum = same ? slots(I3{}, Same{}) : slots(I3{}, Win{});
       } else if (nslots <= 5) {
@@ -406,19 +405,17 @@ __global__ __launch_bounds__(kMhBlock) void mh_sweep_kernel(MhArgs a) {
       sw = me ? P.wn : sw;
       sfx = me ? P.fn : sfx;
       lfx = me ? P.lfn : lfx;
-      const float nph_h = readlane(P.n_ph, 0), nlZ_h = readlane(P.n_lZ, 0);
-      const float nph_w = readlane(P.n_ph, 1), nlZ_w = readlane(P.n_lZ, 1);
-      const float nph_f = readlane(P.n_ph, 2), nlZ_f = readlane(P.n_lZ, 2);
+      const float nph_h = readlane(bph, 3 * b), nlZ_h = readlane(blZ, 3 * b);
+      const float nph_w = readlane(bph, 3 * b + 1), nlZ_w = readlane(blZ, 3 * b + 1);
+      const float nph_f = readlane(bph, 3 * b + 2), nlZ_f = readlane(blZ, 3 * b + 2);
       ph_h = me ? nph_h : ph_h;
       lZ_h = me ? nlZ_h : lZ_h;
       ph_w = me ? nph_w : ph_w;
       lZ_w = me ? nlZ_w : lZ_w;
       ph_f = me ? nph_f : ph_f;
       lZ_f = me ? nlZ_f : lZ_f;
-      // the speculative next proposal read source P.j's old state: redo it
-      if (has_next && Pn.j == P.j) Pn = make_prop((k + 1) & 63);
+      dirty |= 1ull << P.j;
     }
-    P = Pn;
   }
 
   // ---- write back --------------------------------------------------------------
