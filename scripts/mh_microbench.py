@@ -75,6 +75,23 @@ def main():
             torch.cuda.synchronize()
             if r:
                 times[k].append(e0.elapsed_time(e1))
+        # one full render + pixel sum (the loglik kernel) and an MH launch with K=0
+        # and no fresh log-likelihood (launch + staging + one render)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        model.loglikelihood(img, locs, fluxes)
+        e1.record()
+        torch.cuda.synchronize()
+        if r:
+            times.setdefault("loglik_kernel", []).append(e0.elapsed_time(e1))
+        mh0 = p_m71_mh(0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        mh0.run(img, counts, locs, fluxes, tau, prior=prior, image_model=model, want_loglik=False)
+        e1.record()
+        torch.cuda.synchronize()
+        if r:
+            times.setdefault("K=0,no_loglik_out", []).append(e0.elapsed_time(e1))
         # the per-tile launch
         T = nt * nt
         t_ = torch.zeros(T, device=dev)

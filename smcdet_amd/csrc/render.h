@@ -16,7 +16,10 @@ __device__ __forceinline__ int ifloor_clamped(float v) {
   return (int)fmaxf(fminf(floorf(v), 1.0e6f), -1.0e6f);
 }
 
-// lam[p] += amp * psf(|p + 0.5 - (h, w)|) over the source's clipped window
+// lam[p] += amp * psf(|p + 0.5 - (h, w)|) over the source's clipped window.
+// ds_add_f32 (LDS atomic, no return): the adds of one wave to one address are
+// applied in program order, so the sum order is the source order (the result
+// is deterministic) while no add waits for the previous one's read.
 template <int MODEL>
 __device__ __forceinline__ void add_source(const DevModel& m, float* lam, float h, float w,
                                            float amp, int lane) {
@@ -27,17 +30,17 @@ __device__ __forceinline__ void add_source(const DevModel& m, float* lam, float 
   const int bw = c1 - c0 + 1;
   const int npos = (r1 - r0 + 1) * bw;
   const float inv_bw = 1.0f / (float)bw;
-  for (int q = lane; q < npos; q += kWave) {
-    const int a = (int)(((float)q + 0.5f) * inv_bw);
-    const int b = q - a * bw;
-    const int ph = r0 + a, pw = c0 + b;
+  const float ampn = amp * psf_scale<MODEL>(m);
+  for (int q0 = 0; q0 < npos; q0 += kWave) {
+    const int q = q0 + lane;
+    const int aa = (int)(((float)q + 0.5f) * inv_bw);
+    const int bb = q - aa * bw;
+    const int ph = r0 + aa, pw = c0 + bb;
     const float dh = ((float)ph + 0.5f) - h;
     const float dw = ((float)pw + 0.5f) - w;
-    const float r2 = fmaf(dh, dh, dw * dw);
-    const int p = ph * m.W + pw;
-    lam[p] = fmaf(amp, psf_eval<MODEL>(m, r2), lam[p]);
+    const float v = ampn * psf_raw<MODEL>(m, fmaf(dh, dh, dw * dw));
+    if (q < npos) atomicAdd(&lam[ph * m.W + pw], v);
   }
-  wave_sync();
 }
 
 // full render: lam = B + sum_s g*f_s*psf_s ; lane s (< S) holds source s
@@ -51,6 +54,7 @@ __device__ __forceinline__ void render_sources(const DevModel& m, float* lam, fl
     const float h = readlane(sh, s), w = readlane(sw, s), f = readlane(sf, s);
     add_source<MODEL>(m, lam, h, w, m.g * f, lane);
   }
+  wave_sync();
 }
 
 // full render with the catalog read from memory (any S; the per-source loads
@@ -65,6 +69,7 @@ __device__ __forceinline__ void render_sources_mem(const DevModel& m, float* lam
   wave_sync();
   for (int s = 0; s < S; ++s)
     add_source<MODEL>(m, lam, locs[2 * s], locs[2 * s + 1], m.g * fluxes[s], lane);
+  wave_sync();
 }
 
 // sum over pixels of the per-pixel log-likelihood (wave-uniform result);

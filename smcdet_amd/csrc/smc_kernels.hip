@@ -15,8 +15,8 @@
 
 namespace smcdet {
 
-constexpr int kTB = 1024;           // threads per tile workgroup
-constexpr int kTW = kTB / kWave;    // 16 waves
+constexpr int kTB = 256;            // threads per tile workgroup
+constexpr int kTW = kTB / kWave;    // 4 waves
 
 enum : uint32_t { kDoTemper = 1u, kDoWeights = 2u, kDoResample = 4u };
 
@@ -38,67 +38,59 @@ struct TileArgs {
   int64_t* idx;              // [T,N]
 };
 
-// block-wide reductions (1024 threads); red has >= kTW doubles
-__device__ double block_sum(double v, double* red) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  v = wave_sum(v);
-  __syncthreads();
-  if (lane == 0) red[wave] = v;
-  __syncthreads();
-  double s = 0.0;
-  for (int i = 0; i < kTW; ++i) s += red[i];  // fixed order: deterministic
-  __syncthreads();
-  return s;
-}
-__device__ float block_max(float v, float* redf) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  v = wave_max(v);
-  __syncthreads();
-  if (lane == 0) redf[wave] = v;
-  __syncthreads();
-  float s = -INFINITY;
-  for (int i = 0; i < kTW; ++i) s = fmaxf(s, redf[i]);
-  __syncthreads();
-  return s;
-}
-
-// two block sums with ONE barrier: wave DPP sums -> per-wave slots of a
-// double-buffered LDS array -> every thread adds the 16 slots in a fixed
-// order (deterministic, and every thread ends with the same value)
-struct Red2 {
-  double v[2][kTW][2];
+// Workgroup reductions with ONE barrier each: wave DPP reductions -> per-wave
+// slots of a double-buffered LDS array -> every thread combines the kTW slots
+// in a fixed order (deterministic; every thread ends with the same value).
+// `parity` lives in registers and toggles identically in every thread, so a
+// buffer is not rewritten before all threads passed the next call's barrier.
+struct TileRed {
+  double d[2][kTW][2];
+  float f[2][kTW];
 };
-__device__ __forceinline__ void block_sum2(double& a, double& b, Red2* r, int& parity) {
+__device__ __forceinline__ void block_sum2(double& a, double& b, TileRed* r, int& parity) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   a = wave_sum(a);
   b = wave_sum(b);
   const int k = parity;
-  parity ^= 1;  // every thread toggles identically: the next call uses the other buffer
+  parity ^= 1;
   if (lane == 0) {
-    r->v[k][wave][0] = a;
-    r->v[k][wave][1] = b;
+    r->d[k][wave][0] = a;
+    r->d[k][wave][1] = b;
   }
   __syncthreads();
   double sa = 0.0, sb = 0.0;
+#pragma unroll
   for (int i = 0; i < kTW; ++i) {
-    sa += r->v[k][i][0];
-    sb += r->v[k][i][1];
+    sa += r->d[k][i][0];
+    sb += r->d[k][i][1];
   }
   a = sa;
   b = sb;
 }
+__device__ __forceinline__ float block_max(float v, TileRed* r, int& parity) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_max(v);
+  const int k = parity;
+  parity ^= 1;
+  if (lane == 0) r->f[k][wave] = v;
+  __syncthreads();
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < kTW; ++i) m = fmaxf(m, r->f[k][i]);
+  return m;
+}
 
-// f(delta) = ESS(delta) - threshold, evaluated by the whole workgroup:
-// ESS = (sum e)^2 / sum e^2 with e = exp(d*l - max(d*l)), d = float32(delta)
-// (the reference multiplies its float32 log-likelihoods by the python float
-// delta, i.e. at float32 precision; sampler.py:93-97).  Sums in float64.
+// f(delta) = ESS(delta) - threshold, evaluated by the whole workgroup from the
+// LDS-staged log-likelihoods: ESS = (sum e)^2 / sum e^2, e = exp(d*l - max(d*l)),
+// d = float32(delta) (the reference multiplies its float32 log-likelihoods by
+// the python float delta, i.e. at float32 precision; sampler.py:93-97).
 __device__ double block_ess_objective(const float* ll, int N, float lmax, double delta,
-                                      double thr, Red2* red, int& parity) {
+                                      double thr, TileRed* red, int& parity) {
   const float df = (float)delta;
   const float m = df * lmax;  // = max_i fl(df*l_i): rounding is monotone
   double s1 = 0.0, s2 = 0.0;
   for (int i = threadIdx.x; i < N; i += kTB) {
-    const double e = (double)expf(df * ll[i] - m);
+    const double e = (double)fast_exp2((df * ll[i] - m) * kLog2e);
     s1 += e;
     s2 += e * e;
   }
@@ -111,7 +103,7 @@ __device__ double block_ess_objective(const float* ll, int N, float lmax, double
 // 100.  Every thread runs the (deterministic) control flow on identical
 // values; the workgroup evaluates f together.
 __device__ double block_brentq(const float* ll, int N, float lmax, double thr, double xa,
-                               double xb, double fa, double fb, Red2* red, int& parity) {
+                               double xb, double fa, double fb, TileRed* red, int& parity) {
   const double xtol = 1e-6, rtol = 1e-6;
   double xpre = xa, xcur = xb, xblk = 0., fpre = fa, fcur = fb, fblk = 0., spre = 0., scur = 0.;
   if (fpre == 0.0) return xpre;
@@ -159,31 +151,33 @@ __device__ double block_brentq(const float* ll, int N, float lmax, double thr, d
 }
 
 __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
-  extern __shared__ float bins[];  // N floats (resample only)
-  __shared__ double red[kTW];
-  __shared__ float redf[kTW];
-  __shared__ Red2 red2;
+  extern __shared__ float buf[];  // N floats: log-likelihoods, then weights / cumsum
+  __shared__ TileRed red;
   int parity = 0;
   const int t = blockIdx.x;
   const int N = a.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const float* ll = a.loglik + (size_t)t * N;
+
+  if (a.flags & (kDoTemper | kDoWeights)) {
+    const float* llg = a.loglik + (size_t)t * N;
+    for (int i = threadIdx.x; i < N; i += kTB) buf[i] = llg[i];
+    __syncthreads();
+  }
 
   // ------------------------------------------------------------------ temper
   if (a.flags & kDoTemper) {
     const float tau = a.temperature[t];
     float lm = -INFINITY;
-    for (int i = threadIdx.x; i < N; i += kTB) lm = fmaxf(lm, ll[i]);
-    lm = block_max(lm, redf);
+    for (int i = threadIdx.x; i < N; i += kTB) lm = fmaxf(lm, buf[i]);
+    lm = block_max(lm, &red, parity);
     const double top = 1.0 - (double)tau;
     // sampler.py:113-122: root-find only if ESS at delta = 1 - tau is below threshold
-    const double ftop = block_ess_objective(ll, N, lm, top, a.ess_threshold, &red2, parity);
+    const double ftop = block_ess_objective(buf, N, lm, top, a.ess_threshold, &red, parity);
     double delta = top;
     if (ftop < 0.0) {
-      const double f0 = block_ess_objective(ll, N, lm, 0.0, a.ess_threshold, &red2, parity);
-      delta = block_brentq(ll, N, lm, a.ess_threshold, 0.0, top, f0, ftop, &red2, parity);
+      const double f0 = block_ess_objective(buf, N, lm, 0.0, a.ess_threshold, &red, parity);
+      delta = block_brentq(buf, N, lm, a.ess_threshold, 0.0, top, f0, ftop, &red, parity);
     }
-    __syncthreads();
     if (threadIdx.x == 0) {
       const float d32 = (float)delta;  // delta tensor is float32 (sampler.py:105)
       a.temperature_prev[t] = tau;
@@ -197,53 +191,59 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
     const float d = a.temperature[t] - a.temperature_prev[t];
     float mx = -INFINITY;
     for (int i = threadIdx.x; i < N; i += kTB) {
-      const float lw = nan_to_num(d * ll[i], -INFINITY);
+      const float lw = nan_to_num(d * buf[i], -INFINITY);
       a.log_w[(size_t)t * N + i] = lw;
       mx = fmaxf(mx, lw);
     }
-    mx = block_max(mx, redf);
-    double s = 0.0;
-    for (int i = threadIdx.x; i < N; i += kTB) s += (double)expf(a.log_w[(size_t)t * N + i] - mx);
-    s = block_sum(s, red);
+    mx = block_max(mx, &red, parity);
+    double s = 0.0, unused = 0.0;
+    for (int i = threadIdx.x; i < N; i += kTB)
+      s += (double)expf(nan_to_num(d * buf[i], -INFINITY) - mx);
+    block_sum2(s, unused, &red, parity);
     const float sf = (float)s;
     double q = 0.0;
     for (int i = threadIdx.x; i < N; i += kTB) {
-      const float wv = expf(a.log_w[(size_t)t * N + i] - mx) / sf;
+      const float wv = expf(nan_to_num(d * buf[i], -INFINITY) - mx) / sf;
       a.weights[(size_t)t * N + i] = wv;
+      buf[i] = wv;  // same thread, same index: no hazard
       q += (double)wv * (double)wv;
     }
-    q = block_sum(q, red);
+    block_sum2(q, unused, &red, parity);
     if (threadIdx.x == 0) {
       a.ess[t] = (float)(1.0 / q);
       a.logZ[t] = (a.logZ[t] + mx) + logf(sf / (float)N);
     }
-    __syncthreads();
   }
 
   // ---------------------------------------------------------- resample index
   if (a.flags & kDoResample) {
-    const float* W = a.weights + (size_t)t * N;
+    if (!(a.flags & kDoWeights)) {
+      const float* W = a.weights + (size_t)t * N;
+      for (int i = threadIdx.x; i < N; i += kTB) buf[i] = W[i];
+    }
+    __syncthreads();
     // bins = cumsum(W): float64 running sum rounded per element to float32
-    // (what torch's CPU cumsum does), contiguous chunk per thread
+    // (what torch's CPU cumsum does), contiguous chunk per thread, in place
     const int chunk = (N + kTB - 1) / kTB;
-    const int b0 = min(threadIdx.x * chunk, N), b1 = min(b0 + chunk, N);
+    const int b0 = min((int)threadIdx.x * chunk, N), b1 = min(b0 + chunk, N);
     double part = 0.0;
-    for (int i = b0; i < b1; ++i) part += (double)W[i];
-    // exclusive scan of the 1024 chunk sums: wave scan + wave totals
+    for (int i = b0; i < b1; ++i) part += (double)buf[i];
     double incl = part;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const double y = __shfl_up(incl, o, kWave);
       if (lane >= o) incl += y;
     }
-    if (lane == 63) red[wave] = incl;
+    const int k = parity;
+    parity ^= 1;
+    if (lane == 63) red.d[k][wave][0] = incl;
     __syncthreads();
     double base = 0.0;
-    for (int i = 0; i < wave; ++i) base += red[i];
+    for (int i = 0; i < wave; ++i) base += red.d[k][i][0];
     double run = base + incl - part;
     for (int i = b0; i < b1; ++i) {
-      run += (double)W[i];
-      bins[i] = (float)run;
+      run += (double)buf[i];
+      buf[i] = (float)run;
     }
     __syncthreads();
     float U = 0.f;
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
         U = u01(r.x);
       }
     }
-    const float total = bins[N - 1];
+    const float total = buf[N - 1];
     for (int n = threadIdx.x; n < N; n += kTB) {
       int lo = 0, hi = N;  // first i with pred(bins[i])
       if (a.method == SMCDET_RESAMPLE_SYSTEMATIC) {
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
         const float un = ((float)n + U) / (float)N;
         while (lo < hi) {
           const int mid = (lo + hi) >> 1;
-          if (bins[mid] >= un) hi = mid; else lo = mid + 1;
+          if (buf[mid] >= un) hi = mid; else lo = mid + 1;
         }
       } else {
         float un;
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
         const float target = un * total;
         while (lo < hi) {
           const int mid = (lo + hi) >> 1;
-          if (bins[mid] > target) hi = mid; else lo = mid + 1;
+          if (buf[mid] > target) hi = mid; else lo = mid + 1;
         }
       }
       a.idx[(size_t)t * N + n] = (int64_t)min(lo, N - 1);
@@ -335,15 +335,9 @@ __global__ void prune_kernel(const float* __restrict__ locs, const float* __rest
 }
 
 static int launch_tile(const TileArgs& a, hipStream_t st) {
-  size_t lds = 0;
-  if (a.flags & kDoResample) lds = (size_t)a.N * sizeof(float);
-  if (lds > 160 * 1024)
-    return set_error(SMCDET_EUNSUPPORTED, "resampling N=%d exceeds the LDS budget (40960)", a.N);
-  if (lds > 64 * 1024) {
-    if (hipFuncSetAttribute((const void*)tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) != hipSuccess)
-      return set_error(SMCDET_EHIP, "hipFuncSetAttribute failed");
-  }
+  const size_t lds = (size_t)a.N * sizeof(float);
+  int rc = ensure_lds((const void*)tile_kernel, lds + sizeof(TileRed));
+  if (rc) return rc;
   hipLaunchKernelGGL(tile_kernel, dim3(a.T), dim3(kTB), lds, st, a);
   return check_launch("smcdet tile kernel");
 }
