@@ -142,7 +142,9 @@ __device__ __forceinline__ float position_delta(const DevModel& m, const float* 
   return pix_delta<MODEL>(m, xs[p], lgx, lo, dl);
 }
 
-template <int MODEL, bool REPLAY, bool FULL>
+// PPL > 0: tiles of <= 64*PPL pixels rendered in registers (render_regs);
+// PPL = 0: LDS render (larger tiles)
+template <int MODEL, bool REPLAY, bool FULL, int PPL>
 __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   extern __shared__ float smem[];
   const DevModel& m = a.m;
@@ -185,9 +187,17 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   float lfx = fast_log(sfx);
 
   const float tau = a.temperature[t];
-  render_sources<MODEL>(m, lam, sh, sw, sfx, S, lane);
+  double cur_ll;
+  if constexpr (PPL > 0) {
+    float lamk[PPL > 0 ? PPL : 1];
+    render_regs<MODEL, PPL>(m, lamk, sh, sw, sfx, S, lane);
+    cur_ll = pixel_sum_regs<MODEL, PPL>(m, xs, lg, lamk, lane);
+    if constexpr (!FULL) store_regs<MODEL, PPL>(m, lam, lamk, lane);
+  } else {
+    render_sources<MODEL>(m, lam, sh, sw, sfx, S, lane);
+    cur_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
+  }
   lam[HW + lane] = m.bg;
-  double cur_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
 
   // ---- proposals, batched: lane 3b+d proposes dimension d (h, w, flux) of
   // iteration batch_k0 + b (b < kBatch), from the state at batch time.  An
@@ -300,8 +310,14 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
     if constexpr (FULL) {
       const float ch = lane == P.j ? P.hn : sh, cw = lane == P.j ? P.wn : sw;
       const float cf = lane == P.j ? P.fn : sfx;
-      render_sources<MODEL>(m, lam, ch, cw, cf, S, lane);
-      new_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
+      if constexpr (PPL > 0) {
+        float lamk[PPL > 0 ? PPL : 1];
+        render_regs<MODEL, PPL>(m, lamk, ch, cw, cf, S, lane);
+        new_ll = pixel_sum_regs<MODEL, PPL>(m, xs, lg, lamk, lane);
+      } else {
+        render_sources<MODEL>(m, lam, ch, cw, cf, S, lane);
+        new_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
+      }
       dll = (float)(new_ll - cur_ll);
     } else {
       const int fh0 = ifloor_clamped(P.h), fw0 = ifloor_clamped(P.w);
@@ -425,8 +441,15 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
     a.fluxes_out[pid * S + lane] = sfx;
   }
   if (a.loglik_out) {
-    render_sources<MODEL>(m, lam, sh, sw, sfx, S, lane);
-    const double ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
+    double ll;
+    if constexpr (PPL > 0) {
+      float lamk[PPL > 0 ? PPL : 1];
+      render_regs<MODEL, PPL>(m, lamk, sh, sw, sfx, S, lane);
+      ll = pixel_sum_regs<MODEL, PPL>(m, xs, lg, lamk, lane);
+    } else {
+      render_sources<MODEL>(m, lam, sh, sw, sfx, S, lane);
+      ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
+    }
     if (lane == 0) a.loglik_out[pid] = (float)ll;
   }
   if (lane == 0 && accept && a.K > 0) atomicAdd(a.acc_count + t, 1);
@@ -438,23 +461,35 @@ __global__ void acc_finalize_kernel(const int32_t* __restrict__ cnt, int T, int 
   if (t < T) rate[t] = (float)cnt[t] / (float)N;
 }
 
-template <int MODEL, bool REPLAY, bool FULL>
+template <int MODEL, bool REPLAY, bool FULL, int PPL>
 static int launch_mh1(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
-  const void* fn = (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL>;
+  const void* fn = (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL>;
   int rc = ensure_lds(fn, lds);
   if (rc) return rc;
-  hipLaunchKernelGGL((mh_sweep_kernel<MODEL, REPLAY, FULL>), grid, dim3(kMhBlock), lds, st, a);
+  hipLaunchKernelGGL((mh_sweep_kernel<MODEL, REPLAY, FULL, PPL>), grid, dim3(kMhBlock), lds, st,
+                     a);
   return SMCDET_OK;
+}
+
+template <int MODEL, bool REPLAY, bool FULL>
+static int launch_mh_ppl(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
+  const int HW = a.m.H * a.m.W;
+  if (a.S <= kWave) {
+    if (HW <= 64) return launch_mh1<MODEL, REPLAY, FULL, 1>(a, grid, lds, st);
+    if (HW <= 256) return launch_mh1<MODEL, REPLAY, FULL, 4>(a, grid, lds, st);
+    if (HW <= 1024) return launch_mh1<MODEL, REPLAY, FULL, 16>(a, grid, lds, st);
+  }
+  return launch_mh1<MODEL, REPLAY, FULL, 0>(a, grid, lds, st);
 }
 
 template <int MODEL>
 static int launch_mh(const MhArgs& a, bool replay, bool full, dim3 grid, size_t lds,
                      hipStream_t st) {
   if (replay)
-    return full ? launch_mh1<MODEL, true, true>(a, grid, lds, st)
-                : launch_mh1<MODEL, true, false>(a, grid, lds, st);
-  return full ? launch_mh1<MODEL, false, true>(a, grid, lds, st)
-              : launch_mh1<MODEL, false, false>(a, grid, lds, st);
+    return full ? launch_mh_ppl<MODEL, true, true>(a, grid, lds, st)
+                : launch_mh_ppl<MODEL, true, false>(a, grid, lds, st);
+  return full ? launch_mh_ppl<MODEL, false, true>(a, grid, lds, st)
+              : launch_mh_ppl<MODEL, false, false>(a, grid, lds, st);
 }
 
 }  // namespace smcdet

@@ -19,7 +19,7 @@ static size_t model_lds_bytes(const smcdet_image_model_t& m, int per_wave_images
 // ---------------------------------------------------------------------------
 // loglikelihood: one particle per wave, image tile staged in LDS
 // ---------------------------------------------------------------------------
-template <int MODEL>
+template <int MODEL, int PPL>
 __global__ __launch_bounds__(kBlock) void loglik_kernel(DevModel m, const float* __restrict__ img,
                                                         const float* __restrict__ locs,
                                                         const float* __restrict__ fluxes, int N,
@@ -36,8 +36,21 @@ __global__ __launch_bounds__(kBlock) void loglik_kernel(DevModel m, const float*
   const int n = blockIdx.x * kWavesPerBlock + wave;
   if (n >= N) return;
   const size_t pid = (size_t)t * N + n;
-  render_sources_mem<MODEL>(m, lam, locs + pid * S * 2, fluxes + pid * S, S, lane);
-  const double ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
+  double ll;
+  if constexpr (PPL > 0) {
+    float sh = 0.f, sw = 0.f, sf = 0.f;
+    if (lane < S) {
+      sh = locs[(pid * S + lane) * 2 + 0];
+      sw = locs[(pid * S + lane) * 2 + 1];
+      sf = fluxes[pid * S + lane];
+    }
+    float lamk[PPL > 0 ? PPL : 1];
+    render_regs<MODEL, PPL>(m, lamk, sh, sw, sf, S, lane);
+    ll = pixel_sum_regs<MODEL, PPL>(m, xs, lg, lamk, lane);
+  } else {
+    render_sources_mem<MODEL>(m, lam, locs + pid * S * 2, fluxes + pid * S, S, lane);
+    ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
+  }
   if (lane == 0) out[pid] = (float)ll;
 }
 
@@ -241,16 +254,27 @@ int smcdet_loglik(const smcdet_image_model_t* model, const float* tiled_image, c
   const dim3 grid((N + kWavesPerBlock - 1) / kWavesPerBlock, T);
   const size_t lds = model_lds_bytes(*model, 1);
   hipStream_t st = (hipStream_t)stream;
-  rc = ensure_lds(m.model == SMCDET_MODEL_M71 ? (const void*)loglik_kernel<SMCDET_MODEL_M71>
-                                              : (const void*)loglik_kernel<SMCDET_MODEL_POISSON>,
-                  lds);
-  if (rc) return rc;
-  if (m.model == SMCDET_MODEL_M71)
-    hipLaunchKernelGGL(loglik_kernel<SMCDET_MODEL_M71>, grid, dim3(kBlock), lds, st, m,
-                       tiled_image, locs, fluxes, N, S, out);
-  else
-    hipLaunchKernelGGL(loglik_kernel<SMCDET_MODEL_POISSON>, grid, dim3(kBlock), lds, st, m,
-                       tiled_image, locs, fluxes, N, S, out);
+  const int HW = m.H * m.W;
+  const int ppl = S > kWave ? 0 : (HW <= 64 ? 1 : (HW <= 256 ? 4 : (HW <= 1024 ? 16 : 0)));
+#define SMCDET_LL_LAUNCH(MDL, P)                                                            \
+  do {                                                                                       \
+    rc = ensure_lds((const void*)loglik_kernel<MDL, P>, lds);                                \
+    if (rc) return rc;                                                                       \
+    hipLaunchKernelGGL((loglik_kernel<MDL, P>), grid, dim3(kBlock), lds, st, m, tiled_image, \
+                       locs, fluxes, N, S, out);                                             \
+  } while (0)
+  if (m.model == SMCDET_MODEL_M71) {
+    if (ppl == 1) SMCDET_LL_LAUNCH(SMCDET_MODEL_M71, 1);
+    else if (ppl == 4) SMCDET_LL_LAUNCH(SMCDET_MODEL_M71, 4);
+    else if (ppl == 16) SMCDET_LL_LAUNCH(SMCDET_MODEL_M71, 16);
+    else SMCDET_LL_LAUNCH(SMCDET_MODEL_M71, 0);
+  } else {
+    if (ppl == 1) SMCDET_LL_LAUNCH(SMCDET_MODEL_POISSON, 1);
+    else if (ppl == 4) SMCDET_LL_LAUNCH(SMCDET_MODEL_POISSON, 4);
+    else if (ppl == 16) SMCDET_LL_LAUNCH(SMCDET_MODEL_POISSON, 16);
+    else SMCDET_LL_LAUNCH(SMCDET_MODEL_POISSON, 0);
+  }
+#undef SMCDET_LL_LAUNCH
   return check_launch("smcdet_loglik");
 }
 

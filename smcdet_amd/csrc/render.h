@@ -16,10 +16,8 @@ __device__ __forceinline__ int ifloor_clamped(float v) {
   return (int)fmaxf(fminf(floorf(v), 1.0e6f), -1.0e6f);
 }
 
-// lam[p] += amp * psf(|p + 0.5 - (h, w)|) over the source's clipped window.
-// ds_add_f32 (LDS atomic, no return): the adds of one wave to one address are
-// applied in program order, so the sum order is the source order (the result
-// is deterministic) while no add waits for the previous one's read.
+// lam[p] += amp * psf(|p + 0.5 - (h, w)|) over the source's clipped window
+// (LDS read-modify-write; used for tiles above 1024 pixels or S > 64).
 template <int MODEL>
 __device__ __forceinline__ void add_source(const DevModel& m, float* lam, float h, float w,
                                            float amp, int lane) {
@@ -31,16 +29,16 @@ __device__ __forceinline__ void add_source(const DevModel& m, float* lam, float 
   const int npos = (r1 - r0 + 1) * bw;
   const float inv_bw = 1.0f / (float)bw;
   const float ampn = amp * psf_scale<MODEL>(m);
-  for (int q0 = 0; q0 < npos; q0 += kWave) {
-    const int q = q0 + lane;
+  for (int q = lane; q < npos; q += kWave) {
     const int aa = (int)(((float)q + 0.5f) * inv_bw);
     const int bb = q - aa * bw;
     const int ph = r0 + aa, pw = c0 + bb;
     const float dh = ((float)ph + 0.5f) - h;
     const float dw = ((float)pw + 0.5f) - w;
-    const float v = ampn * psf_raw<MODEL>(m, fmaf(dh, dh, dw * dw));
-    if (q < npos) atomicAdd(&lam[ph * m.W + pw], v);
+    const int p = ph * m.W + pw;
+    lam[p] += ampn * psf_raw<MODEL>(m, fmaf(dh, dh, dw * dw));
   }
+  wave_sync();
 }
 
 // full render: lam = B + sum_s g*f_s*psf_s ; lane s (< S) holds source s
@@ -54,7 +52,6 @@ __device__ __forceinline__ void render_sources(const DevModel& m, float* lam, fl
     const float h = readlane(sh, s), w = readlane(sw, s), f = readlane(sf, s);
     add_source<MODEL>(m, lam, h, w, m.g * f, lane);
   }
-  wave_sync();
 }
 
 // full render with the catalog read from memory (any S; the per-source loads
@@ -69,6 +66,75 @@ __device__ __forceinline__ void render_sources_mem(const DevModel& m, float* lam
   wave_sync();
   for (int s = 0; s < S; ++s)
     add_source<MODEL>(m, lam, locs[2 * s], locs[2 * s + 1], m.g * fluxes[s], lane);
+}
+
+// ---------------------------------------------------------------------------
+// Pixel-centric render into registers (tiles of <= 64*PPL pixels): lane owns
+// pixels p = 64k + lane, k < PPL.  Per source only the k-rows its window
+// touches are visited (a wave-uniform range), and the window test is a select,
+// so there is no LDS traffic and no cross-source serialisation.  The sum
+// order per pixel is background, then sources 0..S-1.
+// ---------------------------------------------------------------------------
+template <int MODEL, int PPL>
+__device__ __forceinline__ void render_regs(const DevModel& m, float (&lamk)[PPL], float sh,
+                                            float sw, float sf, int S, int lane) {
+  const int HW = m.H * m.W;
+  const unsigned magic = (65536u + (unsigned)m.W - 1u) / (unsigned)m.W;  // p / W, p < 1024
+#pragma unroll
+  for (int k = 0; k < PPL; ++k) lamk[k] = m.bg;
+  const float scale = m.g * psf_scale<MODEL>(m);
+  for (int s = 0; s < S; ++s) {
+    const float h = readlane(sh, s), w = readlane(sw, s);
+    const float amp = scale * readlane(sf, s);
+    const int fh = ifloor_clamped(h), fw = ifloor_clamped(w);
+    const int r0 = max(fh - m.R, 0), r1 = min(fh + m.R, m.H - 1);
+    if (r0 > r1 || fw + m.R < 0 || fw - m.R > m.W - 1) continue;
+    const int klo = (r0 * m.W) >> 6, khi = ((r1 + 1) * m.W - 1) >> 6;
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+      if (k >= klo && k <= khi) {
+        const int p = k * kWave + lane;
+        const int ph = (int)(__umul24((unsigned)p, magic) >> 16);
+        const int pw = p - ph * m.W;
+        const float dh = ((float)ph + 0.5f) - h;
+        const float dw = ((float)pw + 0.5f) - w;
+        const float v = amp * psf_raw<MODEL>(m, fmaf(dh, dh, dw * dw));
+        const bool in = (unsigned)(ph - fh + m.R) <= 2u * (unsigned)m.R &&
+                        (unsigned)(pw - fw + m.R) <= 2u * (unsigned)m.R && p < HW;
+        lamk[k] += in ? v : 0.0f;
+      }
+    }
+  }
+}
+
+template <int MODEL, int PPL>
+__device__ __forceinline__ double pixel_sum_regs(const DevModel& m, const float* xs,
+                                                 const float* lg, const float (&lamk)[PPL],
+                                                 int lane) {
+  const int HW = m.H * m.W;
+  float acc = 0.0f;
+#pragma unroll
+  for (int k = 0; k < PPL; ++k) {
+    const int p = k * kWave + lane;
+    if (k * kWave < HW) {
+      const int pp = p < HW ? p : 0;
+      const float lgx = (MODEL == SMCDET_MODEL_POISSON) ? lg[pp] : 0.0f;
+      const float e = pix_loglik<MODEL>(m, xs[pp], lgx, lamk[k]);
+      acc += p < HW ? e : 0.0f;
+    }
+  }
+  return wave_sum((double)acc);
+}
+
+template <int MODEL, int PPL>
+__device__ __forceinline__ void store_regs(const DevModel& m, float* lam, const float (&lamk)[PPL],
+                                           int lane) {
+  const int HW = m.H * m.W;
+#pragma unroll
+  for (int k = 0; k < PPL; ++k) {
+    const int p = k * kWave + lane;
+    if (k * kWave < HW && p < HW) lam[p] = lamk[k];
+  }
   wave_sync();
 }
 
