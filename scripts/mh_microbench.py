@@ -58,7 +58,6 @@ def main():
     if a.only:
         variants = {a.only: variants[a.only]}
     times = {k: [] for k in variants}
-    times["tile_kernel"] = []
     mhs = {}
     for k, v in variants.items():
         full, fl = v[0], v[1]
@@ -66,66 +65,51 @@ def main():
         mh.debug_flags = fl
         mhs[k] = mh
     ll = model.loglikelihood(img, locs, fluxes)
+    REP = 5  # back-to-back launches per timing: host launch overhead overlaps GPU work
+
+    def timeit(fn):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(REP):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / REP
+
+    T = nt * nt
+    t_ = torch.zeros(T, device=dev)
+    tp, lw, W = torch.empty(T, device=dev), torch.empty_like(ll), torch.empty_like(ll)
+    ess, lz = torch.empty(T, device=dev), torch.zeros(T, device=dev)
+    idx = torch.empty(ll.shape, device=dev, dtype=torch.int64)
+    mh0 = p_m71_mh(0)
+    extra = {
+        "loglik_kernel": lambda: model.loglikelihood(img, locs, fluxes),
+        "K=0,no_loglik_out": lambda: mh0.run(img, counts, locs, fluxes, tau, prior=prior,
+                                             image_model=model, want_loglik=False),
+        "tile_kernel": lambda: _hip.check(_hip.lib().smcdet_temper_reweight(
+            _hip.ptr(ll), _hip.ptr(torch.zeros(T, device=dev)), _hip.ptr(tp), _hip.ptr(lw),
+            _hip.ptr(W), _hip.ptr(ess), _hip.ptr(lz), T, Np, 0.5 * Np, 1, 1, 0, _hip.ptr(idx),
+            _hip.stream_of(ll)), "tr"),
+        "temper_only": lambda: _hip.check(_hip.lib().smcdet_temper(
+            _hip.ptr(ll), _hip.ptr(torch.zeros(T, device=dev)), _hip.ptr(tp), T, Np, 0.5 * Np,
+            _hip.stream_of(ll)), "t"),
+        "weights_only": lambda: _hip.check(_hip.lib().smcdet_update_weights(
+            _hip.ptr(ll), _hip.ptr(t_), _hip.ptr(tp), _hip.ptr(lw), _hip.ptr(W), _hip.ptr(ess),
+            _hip.ptr(lz), T, Np, _hip.stream_of(ll)), "w"),
+        "resample_only": lambda: _hip.check(_hip.lib().smcdet_resample_index(
+            _hip.ptr(W), T, Np, 1, 1, 0, None, _hip.ptr(idx), _hip.stream_of(ll)), "r"),
+    }
     for r in range(a.rounds + 1):
         for k, mh in mhs.items():
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            mh.run(img, counts, locs, fluxes, tau, prior=prior, image_model=model)
-            e1.record()
-            torch.cuda.synchronize()
+            v = timeit(lambda: mh.run(img, counts, locs, fluxes, tau, prior=prior,
+                                      image_model=model))
             if r:
-                times[k].append(e0.elapsed_time(e1))
-        # one full render + pixel sum (the loglik kernel) and an MH launch with K=0
-        # and no fresh log-likelihood (launch + staging + one render)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        model.loglikelihood(img, locs, fluxes)
-        e1.record()
-        torch.cuda.synchronize()
-        if r:
-            times.setdefault("loglik_kernel", []).append(e0.elapsed_time(e1))
-        mh0 = p_m71_mh(0)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        mh0.run(img, counts, locs, fluxes, tau, prior=prior, image_model=model, want_loglik=False)
-        e1.record()
-        torch.cuda.synchronize()
-        if r:
-            times.setdefault("K=0,no_loglik_out", []).append(e0.elapsed_time(e1))
-        # the per-tile launch
-        T = nt * nt
-        t_ = torch.zeros(T, device=dev)
-        tp, lw, W = torch.empty(T, device=dev), torch.empty_like(ll), torch.empty_like(ll)
-        ess, lz = torch.empty(T, device=dev), torch.zeros(T, device=dev)
-        idx = torch.empty(ll.shape, device=dev, dtype=torch.int64)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        _hip.check(_hip.lib().smcdet_temper_reweight(
-            _hip.ptr(ll), _hip.ptr(t_), _hip.ptr(tp), _hip.ptr(lw), _hip.ptr(W), _hip.ptr(ess),
-            _hip.ptr(lz), T, Np, 0.5 * Np, 1, 1, 0, _hip.ptr(idx), _hip.stream_of(ll)), "tr")
-        e1.record()
-        torch.cuda.synchronize()
-        if r:
-            times["tile_kernel"].append(e0.elapsed_time(e1))
-        # its three parts separately
-        parts = {
-            "temper_only": lambda: _hip.lib().smcdet_temper(
-                _hip.ptr(ll), _hip.ptr(torch.zeros(T, device=dev)), _hip.ptr(tp), T, Np,
-                0.5 * Np, _hip.stream_of(ll)),
-            "weights_only": lambda: _hip.lib().smcdet_update_weights(
-                _hip.ptr(ll), _hip.ptr(t_), _hip.ptr(tp), _hip.ptr(lw), _hip.ptr(W),
-                _hip.ptr(ess), _hip.ptr(lz), T, Np, _hip.stream_of(ll)),
-            "resample_only": lambda: _hip.lib().smcdet_resample_index(
-                _hip.ptr(W), T, Np, 1, 1, 0, None, _hip.ptr(idx), _hip.stream_of(ll)),
-        }
-        for name, fn in parts.items():
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            _hip.check(fn(), name)
-            e1.record()
-            torch.cuda.synchronize()
+                times[k].append(v)
+        for k, fn in extra.items():
+            v = timeit(fn)
             if r:
-                times.setdefault(name, []).append(e0.elapsed_time(e1))
+                times.setdefault(k, []).append(v)
     out = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))}
            for k, v in times.items()}
     steps = nt * nt * Np * a.K

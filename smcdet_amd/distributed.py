@@ -1,0 +1,135 @@
+"""Multi-GPU tile sharding.
+
+Independent image tiles shard embarrassingly: every tensor of the sampler
+leads with the tile dimensions and no operation mixes tiles except the
+reference's global stopping rule (`torch.any(temperature < 1)`,
+smcdet/sampler.py:230).  One process per GPU (torchrun / torch.distributed,
+backend "nccl" = RCCL on ROCm) owns a contiguous block of the row-major tile
+list and runs its own fused SMC loop on it; there is no collective on the
+data path.  Collectives:
+
+* end of run: `gather_catalogs` assembles every rank's per-tile posterior
+  (counts, locs, fluxes, weights, log Z, ESS, iterations, pruned catalogs) on
+  the destination rank (one all_gather of flat float32 buffers per field;
+  ~31 MB for 64 tiles x 4096 particles x 10 sources, well under 1 ms on xGMI);
+* optional lockstep (`lockstep=True`): one 4-byte all_reduce(MAX) per SMC
+  iteration, reproducing the reference's rule that finished tiles keep
+  mutating at temperature 1 until every tile of the image is done.
+
+The default (independent stop per rank) does strictly less work and gives
+each tile the same posterior target.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .sampler import SMCsampler
+
+
+def world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def shard_tiles(num_tiles: int, world_size: int, rank: int):
+    """Contiguous block [start, stop) of the row-major tile list for `rank`;
+    the first num_tiles % world_size ranks get one extra tile."""
+    base, extra = divmod(num_tiles, world_size)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def split_tiles(image: torch.Tensor, tile_dim: int) -> torch.Tensor:
+    """[H, W] image -> [numH*numW, tile, tile] row-major tiles (sampler.py:28-31)."""
+    t = image.unfold(0, tile_dim, tile_dim).unfold(1, tile_dim, tile_dim)
+    return t.reshape(-1, tile_dim, tile_dim)
+
+
+class TileShardedSMC:
+    """SMCsampler over this rank's shard of an image's tiles."""
+
+    def __init__(self, image, tile_dim, Prior, ImageModel, MutationKernel, num_catalogs,
+                 ess_threshold_prop, resample_method, flux_detection_threshold, max_smc_iters,
+                 print_every=10 ** 9, *, lockstep=False, seed=None, device=None, group=None):
+        self.rank, self.world_size = world()
+        self.group = group
+        self.lockstep = lockstep
+        tiles = split_tiles(image, tile_dim)
+        self.num_tiles = tiles.shape[0]
+        self.tiles_per_side = image.shape[0] // tile_dim
+        self.start, self.stop = shard_tiles(self.num_tiles, self.world_size, self.rank)
+        local = tiles[self.start:self.stop]
+        if local.shape[0] == 0:
+            raise ValueError(f"rank {self.rank} has no tiles ({self.num_tiles} tiles, "
+                             f"{self.world_size} ranks)")
+        seed = None if seed is None else int(seed) * 1000003 + self.rank
+        self.sampler = SMCsampler.from_tiles(
+            local.reshape(1, -1, tile_dim, tile_dim), Prior, ImageModel, MutationKernel,
+            num_catalogs, ess_threshold_prop, resample_method, flux_detection_threshold,
+            max_smc_iters, print_every, seed=seed, device=device)
+        if lockstep and self.world_size > 1:
+            self.sampler._keep_going = self._keep_going_global
+
+    def _keep_going_global(self):
+        s = self.sampler
+        flag = (s.temperature < 1).any().to(torch.int32).reshape(1)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        return bool(flag.item())
+
+    def run(self):
+        self.sampler.run()
+        return self
+
+    def local_results(self):
+        s = self.sampler
+        T = s._T
+        out = {
+            "counts": s.counts.reshape(T, -1),
+            "locs": s.locs.reshape(T, *s.locs.shape[2:]),
+            "fluxes": s.fluxes.reshape(T, *s.fluxes.shape[2:]),
+            "weights": s.weights.reshape(T, -1),
+            "log_normalizing_constant": s.log_normalizing_constant.reshape(T),
+            "ess": s.ess.reshape(T),
+            "temperature": s.temperature.reshape(T),
+            "pruned_counts": s.pruned_counts.reshape(T, -1),
+            "pruned_locs": s.pruned_locs.reshape(T, *s.pruned_locs.shape[2:]),
+            "pruned_fluxes": s.pruned_fluxes.reshape(T, *s.pruned_fluxes.shape[2:]),
+            "iter": torch.full((T,), float(s.iter), device=s.device),
+        }
+        return out
+
+    def gather_catalogs(self, dst=0):
+        """All ranks' per-tile results on `dst`, shaped [numH, numW, ...] like
+        the reference's single-process sampler attributes (None elsewhere)."""
+        return gather_tile_results(self.local_results(), self.num_tiles, self.tiles_per_side,
+                                   self.rank, self.world_size, dst=dst, group=self.group)
+
+
+def gather_tile_results(local: dict, num_tiles: int, tiles_per_side: int, rank: int,
+                        world_size: int, dst: int = 0, group=None):
+    """Gathers dicts of [T_local, ...] tensors from every rank into
+    [tiles_per_side, tiles_per_side, ...] tensors on `dst`.  Tensors travel as
+    float32 (integer fields are exact below 2^24) through all_gather on the
+    group's backend (RCCL for GPU tensors, gloo for CPU tensors)."""
+    if world_size == 1:
+        return {k: v.reshape(tiles_per_side, tiles_per_side, *v.shape[1:])
+                for k, v in local.items()}
+    sizes = [shard_tiles(num_tiles, world_size, r) for r in range(world_size)]
+    counts = [b - a for a, b in sizes]
+    tmax = max(counts)
+    out = {}
+    for k in sorted(local):
+        v = local[k]
+        dtype = v.dtype
+        flat = v.reshape(v.shape[0], -1).to(torch.float32)
+        pad = torch.zeros(tmax, flat.shape[1], dtype=torch.float32, device=flat.device)
+        pad[: flat.shape[0]] = flat
+        bufs = [torch.empty_like(pad) for _ in range(world_size)]
+        dist.all_gather(bufs, pad, group=group)
+        if rank == dst:
+            full = torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+            full = full.reshape(num_tiles, *v.shape[1:]).to(dtype)
+            out[k] = full.reshape(tiles_per_side, tiles_per_side, *v.shape[1:])
+    return out if rank == dst else None

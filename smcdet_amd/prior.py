@@ -103,25 +103,27 @@ class PointProcessPrior(object):
         return [counts, locs, fluxes]
 
     def sample_stratified(self, num_tiles_per_side, num_catalogs_per_count, device=None,
-                          rng: PhiloxStream | None = None, uloc=None, uflux=None):
+                          rng: PhiloxStream | None = None, uloc=None, uflux=None,
+                          tiles_shape=None):
         """Stratified draw on device: counts = min..max (each repeated
         num_catalogs_per_count times), uniform locs, prior fluxes, masked past
-        each count.  uloc/uflux replay the reference's torch.rand draws."""
+        each count.  uloc/uflux replay the reference's torch.rand draws.
+        tiles_shape=(numH, numW) overrides the square num_tiles_per_side grid."""
         device = _device(device)
-        T = num_tiles_per_side
+        nH, nW = tiles_shape if tiles_shape is not None else (num_tiles_per_side,) * 2
         N = self.num_counts * num_catalogs_per_count
         S = self.max_objects
-        counts = torch.empty(T, T, N, device=device, dtype=torch.float32)
-        locs = torch.zeros(T, T, N, S, 2, device=device, dtype=torch.float32)
-        fluxes = torch.zeros(T, T, N, S, device=device, dtype=torch.float32)
+        counts = torch.empty(nH, nW, N, device=device, dtype=torch.float32)
+        locs = torch.zeros(nH, nW, N, S, 2, device=device, dtype=torch.float32)
+        fluxes = torch.zeros(nH, nW, N, S, device=device, dtype=torch.float32)
         rng = rng or PhiloxStream()
-        off = rng.take(T * T * N * S)
+        off = rng.take(nH * nW * N * S)
         cp = self._cprior()
         if uloc is not None:
             uloc = _hip.dev_f32(uloc.to(device), "uloc")
             uflux = _hip.dev_f32(uflux.to(device), "uflux")
         _hip.check(_hip.lib().smcdet_prior_sample(
-            _hip.ref(cp), T * T, num_catalogs_per_count, rng.seed, off, _hip.ptr(uloc),
+            _hip.ref(cp), nH * nW, num_catalogs_per_count, rng.seed, off, _hip.ptr(uloc),
             _hip.ptr(uflux), _hip.ptr(counts), _hip.ptr(locs), _hip.ptr(fluxes),
             _hip.stream_of(counts)), "smcdet_prior_sample")
         return counts, locs, fluxes

@@ -42,8 +42,12 @@ class SMCsampler(object):
 
         self.tile_dim = tile_dim
         self.num_tiles_per_side = self.image_dim // self.tile_dim
-        self.tiled_image = (self.image.unfold(0, self.tile_dim, self.tile_dim)
-                            .unfold(1, self.tile_dim, self.tile_dim).contiguous())
+        if image.dim() == 4:  # pre-tiled [numH, numW, tile, tile] (see from_tiles)
+            self.tiled_image = self.image.contiguous()
+        else:
+            self.tiled_image = (self.image.unfold(0, self.tile_dim, self.tile_dim)
+                                .unfold(1, self.tile_dim, self.tile_dim).contiguous())
+        self.tiles_shape = tuple(self.tiled_image.shape[:2])
 
         self.Prior = Prior
         self.ImageModel = ImageModel
@@ -68,14 +72,22 @@ class SMCsampler(object):
         self._fresh_loglik = None   # loglik of the current state, if already known
         self._pending_idx = None    # resampling indices computed by the fused tile launch
 
+    @classmethod
+    def from_tiles(cls, tiles, *args, **kwargs):
+        """A sampler over an explicit [numH, numW, tile, tile] grid of tiles
+        (need not be square or contiguous in the sky: a rank's shard of a
+        larger image, or a batch of independent images)."""
+        if tiles.dim() != 4 or tiles.shape[2] != tiles.shape[3]:
+            raise ValueError("tiles must be [numH, numW, tile, tile]")
+        return cls(tiles, tiles.shape[2], *args, **kwargs)
+
     # ------------------------------------------------------------------ helpers
     @property
     def _T(self):
-        return self.num_tiles_per_side * self.num_tiles_per_side
+        return self.tiles_shape[0] * self.tiles_shape[1]
 
     def _zeros_tiles(self):
-        nt = self.num_tiles_per_side
-        return torch.zeros(nt, nt, device=self.device, dtype=torch.float32)
+        return torch.zeros(*self.tiles_shape, device=self.device, dtype=torch.float32)
 
     def _method_code(self):
         return (_hip.SMCDET_RESAMPLE_SYSTEMATIC if self.resample_method == "systematic"
@@ -87,19 +99,19 @@ class SMCsampler(object):
     # ------------------------------------------------------------ the methods
     def initialize(self):
         """sampler.py:57-85."""
-        nt = self.num_tiles_per_side
+        nH, nW = self.tiles_shape
         self.counts, self.locs, self.fluxes = self.Prior.sample_stratified(
-            nt, self.num_catalogs, device=self.device, rng=self.rng)
+            nH, self.num_catalogs, device=self.device, rng=self.rng, tiles_shape=self.tiles_shape)
         self.Prior.num = self.counts.shape[-1]
         self.temperature_prev = self._zeros_tiles()
         self.temperature = self._zeros_tiles()
         self.loglik = self.ImageModel.loglikelihood(self.tiled_image, self.locs, self.fluxes)
         self._fresh_loglik = self.loglik
         N = self.counts.shape[-1]
-        self.weights_log_unnorm = torch.zeros(nt, nt, N, device=self.device)
-        self.weights = torch.full((nt, nt, N), 1.0 / N, device=self.device)
+        self.weights_log_unnorm = torch.zeros(nH, nW, N, device=self.device)
+        self.weights = torch.full((nH, nW, N), 1.0 / N, device=self.device)
         self.log_normalizing_constant = self._zeros_tiles()
-        self.ess = torch.full((nt, nt), float(N), device=self.device)
+        self.ess = torch.full((nH, nW), float(N), device=self.device)
         self._pending_idx = None
 
     def log_target(self, data, counts, locs, fluxes, temperature):
@@ -237,6 +249,11 @@ class SMCsampler(object):
                         f"{round(acc.max().item(), 2)}]")
             print(msg)
 
+    def _keep_going(self):
+        """sampler.py:230: continue while any tile has temperature < 1 (one
+        device->host read per SMC iteration)."""
+        return bool((self.temperature < 1).any())
+
     def run(self):
         """sampler.py:221-256."""
         self.iter = 0
@@ -244,7 +261,7 @@ class SMCsampler(object):
         self.initialize()
         if self.fused:
             self._temper_reweight(with_resample=True)
-            while bool((self.temperature < 1).any()) and self.iter <= self.max_smc_iters:
+            while self._keep_going() and self.iter <= self.max_smc_iters:
                 self.iter += 1
                 self._print_progress()
                 idx, self._pending_idx = self._pending_idx, None
@@ -253,7 +270,7 @@ class SMCsampler(object):
         else:
             self.temper()
             self.update_weights()
-            while bool((self.temperature < 1).any()) and self.iter <= self.max_smc_iters:
+            while self._keep_going() and self.iter <= self.max_smc_iters:
                 self.iter += 1
                 self._print_progress()
                 self.resample()

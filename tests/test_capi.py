@@ -1,0 +1,61 @@
+"""The C-ABI library loads on a host without a GPU and exports every entry
+point include/smcdet_hip.h declares; the ctypes structs match the header
+layout; argument validation fails loudly (no compute is launched)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from smcdet_amd import _hip
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "smcdet_hip.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(smcdet_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_every_header_symbol_is_exported_and_bound():
+    names = header_functions()
+    assert len(names) >= 15
+    L = _hip.lib()
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(_hip.EXPORTS), set(names) ^ set(_hip.EXPORTS)
+
+
+def test_version_and_abi():
+    assert _hip.lib().smcdet_abi_version() == 1
+    assert "gfx950" in _hip.version()
+
+
+def test_struct_layouts_match_header():
+    # sizes of the POD structs as the header declares them (all 4-byte fields)
+    assert ctypes.sizeof(_hip.ImageModelC) == 4 * 4 + 4 * 2 + 6 * 4 + 3 * 4
+    assert ctypes.sizeof(_hip.PriorC) == 3 * 4 + 7 * 4
+    assert ctypes.sizeof(_hip.MHC) == 4 + 8 * 4
+    assert ctypes.sizeof(_hip.ReplayC) == 4 * ctypes.sizeof(ctypes.c_void_p)
+
+
+def test_invalid_arguments_fail_loudly_without_gpu():
+    L = _hip.lib()
+    rc = L.smcdet_loglik(None, None, None, None, 1, 1, 1, None, None)
+    assert rc == -1
+    assert b"null" in L.smcdet_last_error()
+    m = _hip.ImageModelC()
+    m.model, m.H, m.W, m.psf_radius = 1, 100, 100, 8  # 10,000 px > 4,096
+    rc = L.smcdet_loglik(ctypes.byref(m), ctypes.c_void_p(1), ctypes.c_void_p(1),
+                         ctypes.c_void_p(1), 1, 1, 1, ctypes.c_void_p(1), None)
+    assert rc == -2
+    with pytest.raises(RuntimeError, match="failed"):
+        _hip.check(rc, "smcdet_loglik")
+
+
+def test_product_refuses_host_tensors():
+    import torch
+    with pytest.raises(RuntimeError, match="HIP device"):
+        _hip.dev_f32(torch.zeros(3), "x")
