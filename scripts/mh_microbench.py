@@ -83,6 +83,7 @@ def main():
     ess, lz = torch.empty(T, device=dev), torch.zeros(T, device=dev)
     idx = torch.empty(ll.shape, device=dev, dtype=torch.int64)
     mh0 = p_m71_mh(0)
+    ll64 = ll[..., :64].contiguous()
     extra = {
         "loglik_kernel": lambda: model.loglikelihood(img, locs, fluxes),
         "K=0,no_loglik_out": lambda: mh0.run(img, counts, locs, fluxes, tau, prior=prior,
@@ -94,6 +95,9 @@ def main():
         "temper_only": lambda: _hip.check(_hip.lib().smcdet_temper(
             _hip.ptr(ll), _hip.ptr(torch.zeros(T, device=dev)), _hip.ptr(tp), T, Np, 0.5 * Np,
             _hip.stream_of(ll)), "t"),
+        "temper_only_N64": lambda: _hip.check(_hip.lib().smcdet_temper(
+            _hip.ptr(ll64), _hip.ptr(torch.zeros(T, device=dev)), _hip.ptr(tp), T, 64, 32.0,
+            _hip.stream_of(ll)), "t64"),
         "weights_only": lambda: _hip.check(_hip.lib().smcdet_update_weights(
             _hip.ptr(ll), _hip.ptr(t_), _hip.ptr(tp), _hip.ptr(lw), _hip.ptr(W), _hip.ptr(ess),
             _hip.ptr(lz), T, Np, _hip.stream_of(ll)), "w"),

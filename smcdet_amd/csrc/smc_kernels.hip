@@ -3,20 +3,24 @@
 // systematic and multinomial resampling (sampler.py:127-169) and pruning
 // (sampler.py:198-219).
 //
-// One 1024-thread workgroup per tile does temper -> reweight -> resample
+// One 256-thread workgroup per tile does temper -> reweight -> resample
 // indices in one launch, so an SMC iteration needs no host round trip (the
 // reference copies the log-likelihoods to the host and runs scipy brentq per
-// tile).  The tempering root is found by the same Brent iteration as scipy's
-// brentq (so the same root is picked when ESS(delta) crosses the threshold
-// more than once), each f evaluation being a workgroup-wide reduction.
+// tile).  ESS(delta) is monotone, but brentq stops within xtol = 1e-6 of the
+// root, which early in a run is as large as delta itself: the tempering
+// schedule (and so the iteration count) is brentq's, not the exact root's.
+// The root is therefore found by the same Brent iteration as scipy's brentq,
+// each f evaluation being a workgroup-wide reduction.
 #include <math.h>
 
 #include "device.h"
 
 namespace smcdet {
 
-constexpr int kTB = 256;            // threads per tile workgroup
-constexpr int kTW = kTB / kWave;    // 4 waves
+constexpr int kTB = 512;            // threads per tile workgroup
+constexpr int kTW = kTB / kWave;    // 8 waves (2 per SIMD)
+constexpr int kMaxPer = 32;         // log-likelihoods per thread held in registers
+constexpr int kMaxN = kTB * kMaxPer;
 
 enum : uint32_t { kDoTemper = 1u, kDoWeights = 2u, kDoResample = 4u };
 
@@ -46,6 +50,8 @@ struct TileArgs {
 struct TileRed {
   double d[2][kTW][2];
   float f[2][kTW];
+  float f2[2][kTW][2];
+  int i[2][kTW];
 };
 __device__ __forceinline__ void block_sum2(double& a, double& b, TileRed* r, int& parity) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -67,6 +73,34 @@ __device__ __forceinline__ void block_sum2(double& a, double& b, TileRed* r, int
   a = sa;
   b = sb;
 }
+__device__ __forceinline__ void block_sum2f(float& a, float& b, TileRed* r, int& parity) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int k = parity;
+  parity ^= 1;
+  if (lane == 0) {
+    r->f2[k][wave][0] = a;
+    r->f2[k][wave][1] = b;
+  }
+  __syncthreads();
+  float sa[kTW], sb[kTW];
+#pragma unroll
+  for (int i = 0; i < kTW; ++i) {
+    sa[i] = r->f2[k][i][0];
+    sb[i] = r->f2[k][i][1];
+  }
+#pragma unroll
+  for (int w = 1; w < kTW; w <<= 1) {
+#pragma unroll
+    for (int i = 0; i + w < kTW; i += 2 * w) {
+      sa[i] += sa[i + w];
+      sb[i] += sb[i + w];
+    }
+  }
+  a = sa[0];
+  b = sb[0];
+}
 __device__ __forceinline__ float block_max(float v, TileRed* r, int& parity) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   v = wave_max(v);
@@ -80,30 +114,61 @@ __device__ __forceinline__ float block_max(float v, TileRed* r, int& parity) {
   return m;
 }
 
-// f(delta) = ESS(delta) - threshold, evaluated by the whole workgroup from the
-// LDS-staged log-likelihoods: ESS = (sum e)^2 / sum e^2, e = exp(d*l - max(d*l)),
-// d = float32(delta) (the reference multiplies its float32 log-likelihoods by
-// the python float delta, i.e. at float32 precision; sampler.py:93-97).
-__device__ double block_ess_objective(const float* ll, int N, float lmax, double delta,
-                                      double thr, TileRed* red, int& parity) {
+// Pairwise (depth log2 PER) sum of a register array: short dependency chains,
+// which is what a one-workgroup-per-tile kernel with nothing to hide latency
+// behind needs.
+template <class V, int PER>
+__device__ __forceinline__ V tree_sum(V (&x)[PER]) {
+#pragma unroll
+  for (int w = 1; w < PER; w <<= 1) {
+#pragma unroll
+    for (int j = 0; j + w < PER; j += 2 * w) x[j] += x[j + w];
+  }
+  return x[0];
+}
+
+// Each thread's log-likelihoods (i = threadIdx.x + j*kTB) live in registers
+// for the whole tempering search.
+template <int PER>
+struct TileLL {
+  float l[PER];
+  __device__ __forceinline__ bool valid(int j, int N) const {
+    return (int)threadIdx.x + j * kTB < N;
+  }
+};
+
+// f(delta) = ESS(delta) - threshold: ESS = (sum e)^2 / sum e^2,
+// e = exp(d*l - max(d*l)), d = float32(delta) (the reference multiplies its
+// float32 log-likelihoods by the python float delta and reduces in float32;
+// sampler.py:93-97).  Sums are float32 pairwise trees (relative error ~1e-6,
+// the reference's own float32 logsumexp level); only the ratio is double.
+// This sits on the latency-bound path of every Brent iteration, so it is
+// short: one exp per element, float DPP reductions, one barrier.
+template <int PER>
+__device__ __forceinline__ double block_ess_objective(const TileLL<PER>& ll, int N, float lmax,
+                                                      double delta, double thr, TileRed* red,
+                                                      int& parity) {
   const float df = (float)delta;
   const float m = df * lmax;  // = max_i fl(df*l_i): rounding is monotone
-  double s1 = 0.0, s2 = 0.0;
-  for (int i = threadIdx.x; i < N; i += kTB) {
-    const double e = (double)fast_exp2((df * ll[i] - m) * kLog2e);
-    s1 += e;
-    s2 += e * e;
+  float e1[PER], e2[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const float e = ll.valid(j, N) ? fast_exp2((df * ll.l[j] - m) * kLog2e) : 0.f;
+    e1[j] = e;
+    e2[j] = e * e;
   }
-  block_sum2(s1, s2, red, parity);
-  return s1 * s1 / s2 - thr;
+  float s1 = tree_sum(e1), s2 = tree_sum(e2);
+  block_sum2f(s1, s2, red, parity);
+  const double d1 = (double)s1;
+  return d1 * d1 / (double)s2 - thr;
 }
 
 // scipy.optimize.brentq (scipy/optimize/Zeros/brentq.c, the algorithm the
 // reference calls at sampler.py:114-120) with xtol = rtol = 1e-6, maxiter
 // 100.  Every thread runs the (deterministic) control flow on identical
 // values; the workgroup evaluates f together.
-__device__ double block_brentq(const float* ll, int N, float lmax, double thr, double xa,
-                               double xb, double fa, double fb, TileRed* red, int& parity) {
+template <class F>
+__device__ double block_brentq(F&& f, double xa, double xb, double fa, double fb) {
   const double xtol = 1e-6, rtol = 1e-6;
   double xpre = xa, xcur = xb, xblk = 0., fpre = fa, fcur = fb, fblk = 0., spre = 0., scur = 0.;
   if (fpre == 0.0) return xpre;
@@ -145,72 +210,91 @@ __device__ double block_brentq(const float* ll, int N, float lmax, double thr, d
     fpre = fcur;
     if (fabs(scur) > delta) xcur += scur;
     else xcur += (sbis > 0 ? delta : -delta);
-    fcur = block_ess_objective(ll, N, lmax, xcur, thr, red, parity);
+    fcur = f(xcur);
   }
   return xcur;
 }
 
+template <int PER>
 __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
-  extern __shared__ float buf[];  // N floats: log-likelihoods, then weights / cumsum
+  extern __shared__ float buf[];  // N floats: weights / cumsum, then N+1 resample slots
   __shared__ TileRed red;
   int parity = 0;
   const int t = blockIdx.x;
   const int N = a.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
+  TileLL<PER> ll;
   if (a.flags & (kDoTemper | kDoWeights)) {
     const float* llg = a.loglik + (size_t)t * N;
-    for (int i = threadIdx.x; i < N; i += kTB) buf[i] = llg[i];
-    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) ll.l[j] = ll.valid(j, N) ? llg[threadIdx.x + j * kTB] : 0.f;
   }
 
   // ------------------------------------------------------------------ temper
+  float d_new = 0.f;  // float32 temperature increment, when tempered here
   if (a.flags & kDoTemper) {
     const float tau = a.temperature[t];
     float lm = -INFINITY;
-    for (int i = threadIdx.x; i < N; i += kTB) lm = fmaxf(lm, buf[i]);
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      if (ll.valid(j, N)) lm = fmaxf(lm, ll.l[j]);
     lm = block_max(lm, &red, parity);
+    const double thr = a.ess_threshold;
+    auto f = [&](double x) { return block_ess_objective(ll, N, lm, x, thr, &red, parity); };
     const double top = 1.0 - (double)tau;
     // sampler.py:113-122: root-find only if ESS at delta = 1 - tau is below threshold
-    const double ftop = block_ess_objective(buf, N, lm, top, a.ess_threshold, &red, parity);
+    const double ftop = f(top);
     double delta = top;
-    if (ftop < 0.0) {
-      const double f0 = block_ess_objective(buf, N, lm, 0.0, a.ess_threshold, &red, parity);
-      delta = block_brentq(buf, N, lm, a.ess_threshold, 0.0, top, f0, ftop, &red, parity);
-    }
+    // f(0) = N - thr exactly: every weight is exp(0) = 1
+    if (ftop < 0.0) delta = block_brentq(f, 0.0, top, (double)N - thr, ftop);
+    const float tnew = tau + (float)delta;  // delta tensor is float32 (sampler.py:105)
+    d_new = tnew - tau;
     if (threadIdx.x == 0) {
-      const float d32 = (float)delta;  // delta tensor is float32 (sampler.py:105)
       a.temperature_prev[t] = tau;
-      a.temperature[t] = tau + d32;
+      a.temperature[t] = tnew;
     }
-    __syncthreads();
   }
 
   // ------------------------------------------------------------ update weights
   if (a.flags & kDoWeights) {
-    const float d = a.temperature[t] - a.temperature_prev[t];
+    const float d = (a.flags & kDoTemper) ? d_new : a.temperature[t] - a.temperature_prev[t];
+    float* lwg = a.log_w + (size_t)t * N;
+    float* wg = a.weights + (size_t)t * N;
+    float e[PER];
     float mx = -INFINITY;
-    for (int i = threadIdx.x; i < N; i += kTB) {
-      const float lw = nan_to_num(d * buf[i], -INFINITY);
-      a.log_w[(size_t)t * N + i] = lw;
-      mx = fmaxf(mx, lw);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      e[j] = nan_to_num(d * ll.l[j], -INFINITY);
+      if (ll.valid(j, N)) {
+        lwg[threadIdx.x + j * kTB] = e[j];
+        mx = fmaxf(mx, e[j]);
+      }
     }
     mx = block_max(mx, &red, parity);
-    double s = 0.0, unused = 0.0;
-    for (int i = threadIdx.x; i < N; i += kTB)
-      s += (double)expf(nan_to_num(d * buf[i], -INFINITY) - mx);
-    block_sum2(s, unused, &red, parity);
-    const float sf = (float)s;
-    double q = 0.0;
-    for (int i = threadIdx.x; i < N; i += kTB) {
-      const float wv = expf(nan_to_num(d * buf[i], -INFINITY) - mx) / sf;
-      a.weights[(size_t)t * N + i] = wv;
-      buf[i] = wv;  // same thread, same index: no hazard
-      q += (double)wv * (double)wv;
+    double s[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      e[j] = ll.valid(j, N) ? expf(e[j] - mx) : 0.f;
+      s[j] = (double)e[j];
     }
-    block_sum2(q, unused, &red, parity);
+    double ssum = tree_sum(s), unused = 0.0;
+    block_sum2(ssum, unused, &red, parity);
+    const float sf = (float)ssum;
+    double q[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const float wv = e[j] / sf;
+      q[j] = (double)wv * (double)wv;
+      if (ll.valid(j, N)) {
+        wg[threadIdx.x + j * kTB] = wv;
+        buf[threadIdx.x + j * kTB] = wv;
+      }
+    }
+    double qs = tree_sum(q);
+    block_sum2(qs, unused, &red, parity);
     if (threadIdx.x == 0) {
-      a.ess[t] = (float)(1.0 / q);
+      a.ess[t] = (float)(1.0 / qs);
       a.logZ[t] = (a.logZ[t] + mx) + logf(sf / (float)N);
     }
   }
@@ -257,16 +341,60 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
       }
     }
     const float total = buf[N - 1];
-    for (int n = threadIdx.x; n < N; n += kTB) {
-      int lo = 0, hi = N;  // first i with pred(bins[i])
-      if (a.method == SMCDET_RESAMPLE_SYSTEMATIC) {
-        // u = (n + U) / N in float32 (sampler.py:144); bucketize right=False
-        const float un = ((float)n + U) / (float)N;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (buf[mid] >= un) hi = mid; else lo = mid + 1;
+    int64_t* idxg = a.idx + (size_t)t * N;
+    if (a.method == SMCDET_RESAMPLE_SYSTEMATIC) {
+      // bucketize(u, bins), u_n = (n + U) / N in float32 (sampler.py:144),
+      // right=False: idx[n] = #{i : bins[i] < u_n}.  With cnt(i) = #{n : u_n <= bins[i]}
+      // (monotone in i), idx[n] = #{i : cnt(i) <= n}: the last bin of every run of
+      // equal cnt writes i+1 to slot[cnt], and a prefix max over slots gives idx.
+      // Exact (u_n is recomputed with the same float ops) and load-balanced
+      // whatever the weight degeneracy, unlike a per-n search.
+      int* slot = reinterpret_cast<int*>(buf + N);  // N+1 ints
+      const float Nf = (float)N;
+      auto un = [&](int n) { return ((float)n + U) / Nf; };
+      auto cnt = [&](float b) {
+        int c = (int)fminf(fmaxf(floorf(b * Nf - U), 0.f), Nf);
+        while (c > 0 && un(c - 1) > b) --c;
+        while (c < N && un(c) <= b) ++c;
+        return c;
+      };
+      for (int i = threadIdx.x; i <= N; i += kTB) slot[i] = 0;
+      __syncthreads();
+      if (b0 < b1) {
+        int cprev = cnt(buf[b0]);
+        for (int i = b0; i < b1; ++i) {
+          const int cnext = (i + 1 < N) ? cnt(buf[i + 1]) : -1;
+          if (cnext != cprev) slot[cprev] = i + 1;
+          cprev = cnext;
         }
-      } else {
+      }
+      __syncthreads();
+      // prefix max over slot[0..N-1], contiguous chunk per thread
+      int pm = 0;
+      for (int i = b0; i < b1; ++i) pm = max(pm, slot[i]);
+      int incl_m = pm;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl_m, o, kWave);
+        if (lane >= o) incl_m = max(incl_m, y);
+      }
+      const int k2 = parity;
+      parity ^= 1;
+      if (lane == 63) red.i[k2][wave] = incl_m;
+      __syncthreads();
+      int run_m = __shfl_up(incl_m, 1, kWave);
+      if (lane == 0) run_m = 0;
+      for (int i = 0; i < wave; ++i) run_m = max(run_m, red.i[k2][i]);
+      // in place: slot[i] becomes idx[i] (each thread owns its chunk)
+      for (int i = b0; i < b1; ++i) {
+        run_m = max(run_m, slot[i]);
+        slot[i] = min(run_m, N - 1);
+      }
+      __syncthreads();
+      for (int n = threadIdx.x; n < N; n += kTB) idxg[n] = (int64_t)slot[n];
+    } else {
+      // multinomial (sampler.py:127-140): target = u * total, first bin > target
+      for (int n = threadIdx.x; n < N; n += kTB) {
         float un;
         if (a.u) {
           un = a.u[(size_t)t * N + n];
@@ -277,12 +405,13 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
           un = u01(r.x);
         }
         const float target = un * total;
+        int lo = 0, hi = N;
         while (lo < hi) {
           const int mid = (lo + hi) >> 1;
           if (buf[mid] > target) hi = mid; else lo = mid + 1;
         }
+        idxg[n] = (int64_t)min(lo, N - 1);
       }
-      a.idx[(size_t)t * N + n] = (int64_t)min(lo, N - 1);
     }
   }
 }
@@ -335,10 +464,22 @@ __global__ void prune_kernel(const float* __restrict__ locs, const float* __rest
 }
 
 static int launch_tile(const TileArgs& a, hipStream_t st) {
-  const size_t lds = (size_t)a.N * sizeof(float);
-  int rc = ensure_lds((const void*)tile_kernel, lds + sizeof(TileRed));
+  if (a.N > kMaxN)
+    return set_error(SMCDET_EUNSUPPORTED, "N=%d particles per tile > %d", a.N, kMaxN);
+  // weights / bins, then (systematic resampling) N+1 slots
+  const size_t lds = (size_t)(2 * a.N + 1) * sizeof(float);
+  const int per = (a.N + kTB - 1) / kTB;
+  const void* fn = per <= 1 ? (const void*)tile_kernel<1>
+                 : per <= 2 ? (const void*)tile_kernel<2>
+                 : per <= 4 ? (const void*)tile_kernel<4>
+                 : per <= 8 ? (const void*)tile_kernel<8>
+                 : per <= 16 ? (const void*)tile_kernel<16>
+                             : (const void*)tile_kernel<32>;
+  int rc = ensure_lds(fn, lds + sizeof(TileRed));
   if (rc) return rc;
-  hipLaunchKernelGGL(tile_kernel, dim3(a.T), dim3(kTB), lds, st, a);
+  void* args[] = {const_cast<TileArgs*>(&a)};
+  hipError_t e = hipLaunchKernel(fn, dim3(a.T), dim3(kTB), args, lds, st);
+  if (e != hipSuccess) return set_error(SMCDET_EHIP, "tile kernel launch: %s", hipGetErrorString(e));
   return check_launch("smcdet tile kernel");
 }
 
