@@ -46,6 +46,7 @@ HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md (spec)
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md (vector FP32, spec)
 B_ALG_PER_STEP = 248        # SURVEY §8d, S=10
 F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
+PMC_FILE = "pmc_mh_r01.json"  # rocprofv3 FETCH_SIZE+WRITE_SIZE per MH launch (scripts/profile.sh)
 
 
 def parse():
@@ -168,27 +169,25 @@ def main():
 
     ev = []
 
-    def step(record):
+    def step():
         idx, s._pending_idx = s._pending_idx, None
-        if record:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
         s.mutate(ancestors=idx)
-        if record:
-            e1.record()
-            ev.append((e0, e1))
         s._temper_reweight(with_resample=True)
 
     for _ in range(args.warmup):
-        step(False)
+        step()
+    # HIP events recorded on the launch stream right around each MH sweep
+    # launch (smcdet_mh_sweep = one kernel): the roofline's kernel duration
+    mh.launch_events = ev
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(True)
+        step()
     torch.cuda.synchronize()
+    mh.launch_events = None
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
@@ -205,7 +204,7 @@ def main():
     achieved_gbs = B_ALG_PER_STEP * launch_steps / (mh_ms * 1e-3) / 1e9
     mh_rate = launch_steps / (mh_ms * 1e-3)
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_mh_r01.json")
+    pmc = os.path.join(ROOT, "profiles", PMC_FILE)
     if os.path.exists(pmc):
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")

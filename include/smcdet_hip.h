@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 1
+#define SMCDET_ABI_VERSION 2
 
 /* status codes */
 #define SMCDET_OK 0
@@ -145,7 +145,10 @@ int smcdet_prior_sample(const smcdet_prior_t* prior, int32_t T,
  * be null.  temperature[T].  Outputs: acc_rate[T] = acceptance rate of the
  * LAST iteration (kernel.py:130); loglik_out[T,N] (nullable) = the image
  * log-likelihood of the returned state (what SMCsampler.temper recomputes,
- * sampler.py:100-102).  acc_count[T] is an int32 workspace. */
+ * sampler.py:100-102).  acc_count[2T] is an int32 workspace that must be
+ * zero before the first call; every call leaves it zero again (it holds the
+ * per-tile accept counters and workgroup tickets only while the kernel runs),
+ * so one zeroed buffer serves every call on a stream. */
 int smcdet_mh_sweep(const smcdet_image_model_t* model,
                     const smcdet_prior_t* prior, const smcdet_mh_t* mh,
                     const float* tiled_image, const float* temperature,

@@ -25,8 +25,9 @@
 //     whose error scales with the change, not with the absolute terms.  (Mode SMCDET_MH_FULL_RECOMPUTE instead
 //     re-renders every source each step, as the reference does.)
 //   * accept iff U <= min(1, exp(log alpha)) (kernel.py:114-116).
-// The rate image is rebuilt from scratch at the start of each sweep and the
-// returned loglik_out comes from a fresh full render of the final state.
+// The rate image is rebuilt from scratch at the start of each sweep; the
+// returned loglik_out is summed over the final rate image (fresh full render
+// in FULL_RECOMPUTE mode).
 #include <math.h>
 
 #include <type_traits>
@@ -60,7 +61,8 @@ struct MhArgs {
   float* locs_out;
   float* fluxes_out;
   float* loglik_out;                 // [T,N] or null
-  int32_t* acc_count;                // [T]
+  int32_t* acc_count;                // [2T] zeroed workspace: counts, tickets
+  float* acc_rate;                   // [T]
   const int32_t* r_comp;             // replay (or null)
   const float* r_uloc;
   const float* r_uflux;
@@ -147,6 +149,7 @@ __device__ __forceinline__ float position_delta(const DevModel& m, const float* 
 template <int MODEL, bool REPLAY, bool FULL, int PPL>
 __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   extern __shared__ float smem[];
+  __shared__ int wg_acc, wg_done;  // last-iteration accepts / finished waves of this workgroup
   const DevModel& m = a.m;
   const int HW = m.H * m.W;
   const int HWp = HW + kWave;  // + one dummy cell per lane (HW + lane) for masked lanes
@@ -158,6 +161,10 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   float* lam = smem + kImg * HWp + wave * HWp;
 
   stage_image<MODEL>(a.img + (size_t)t * HW, xs, lg, HW, threadIdx.x, kMhBlock);
+  if (threadIdx.x == 0) {
+    wg_acc = 0;
+    wg_done = 0;
+  }
   if (threadIdx.x < kWave) {
     xs[HW + threadIdx.x] = m.bg;
     if (MODEL == SMCDET_MODEL_POISSON) lg[HW + threadIdx.x] = 0.f;
@@ -442,7 +449,11 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   }
   if (a.loglik_out) {
     double ll;
-    if constexpr (PPL > 0) {
+    if constexpr (!FULL) {
+      // the LDS rate image is current (every accepted move was applied to it):
+      // sum the per-pixel terms over it instead of re-rendering all sources
+      ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
+    } else if constexpr (PPL > 0) {
       float lamk[PPL > 0 ? PPL : 1];
       render_regs<MODEL, PPL>(m, lamk, sh, sw, sfx, S, lane);
       ll = pixel_sum_regs<MODEL, PPL>(m, xs, lg, lamk, lane);
@@ -452,13 +463,26 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
     }
     if (lane == 0) a.loglik_out[pid] = (float)ll;
   }
-  if (lane == 0 && accept && a.K > 0) atomicAdd(a.acc_count + t, 1);
-}
-
-__global__ void acc_finalize_kernel(const int32_t* __restrict__ cnt, int T, int N,
-                                    float* __restrict__ rate) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < T) rate[t] = (float)cnt[t] / (float)N;
+  // ---- acceptance rate of the last iteration (kernel.py:130), no extra launch:
+  // waves add into LDS; the workgroup's last wave adds the total to the tile's
+  // counter and takes a ticket; the tile's last workgroup writes the rate and
+  // re-zeroes counter and ticket (the workspace is zero on entry and exit).
+  if (lane == 0) {
+    const int nw = min(kMhWaves, N - (int)blockIdx.x * kMhWaves);
+    if (accept && a.K > 0) atomicAdd(&wg_acc, 1);
+    __threadfence_block();
+    if (atomicAdd(&wg_done, 1) == nw - 1) {
+      int32_t* cnt = a.acc_count + t;
+      int32_t* ticket = a.acc_count + a.T + t;
+      atomicAdd(cnt, atomicAdd(&wg_acc, 0));
+      __threadfence();
+      if (atomicAdd(ticket, 1) == (int)gridDim.x - 1) {
+        const int total = atomicExch(cnt, 0);
+        atomicExch(ticket, 0);
+        a.acc_rate[t] = (float)total / (float)N;
+      }
+    }
+  }
 }
 
 template <int MODEL, bool REPLAY, bool FULL, int PPL>
@@ -555,6 +579,7 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
   a.fluxes_out = fluxes_out;
   a.loglik_out = loglik_out;
   a.acc_count = acc_count;
+  a.acc_rate = acc_rate;
   if (replay) {
     a.r_comp = replay->comp;
     a.r_uloc = replay->uloc;
@@ -562,8 +587,6 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
     a.r_uacc = replay->uacc;
   }
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(acc_count, 0, (size_t)T * sizeof(int32_t), st) != hipSuccess)
-    return set_error(SMCDET_EHIP, "smcdet_mh_sweep: memset failed");
   const size_t HWp = (size_t)model->H * model->W + kWave;
   const size_t lds =
       ((model->model == SMCDET_MODEL_POISSON ? 2 : 1) * HWp + (size_t)kMhWaves * HWp) *
@@ -575,9 +598,5 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
            ? launch_mh<SMCDET_MODEL_M71>(a, replay != nullptr, full, grid, lds, st)
            : launch_mh<SMCDET_MODEL_POISSON>(a, replay != nullptr, full, grid, lds, st);
   if (rc) return rc;
-  rc = check_launch("smcdet_mh_sweep");
-  if (rc) return rc;
-  hipLaunchKernelGGL(acc_finalize_kernel, dim3((T + 255) / 256), dim3(256), 0, st, acc_count, T,
-                     N, acc_rate);
-  return check_launch("smcdet_mh_sweep(finalize)");
+  return check_launch("smcdet_mh_sweep");
 }

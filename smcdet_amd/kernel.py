@@ -39,6 +39,8 @@ class SingleComponentMH(object):
         self.rng = None           # PhiloxStream; SMCsampler installs its own
         self.debug_flags = 0      # SMCDET_MH_ABLATE_* timing diagnostics (never for sampling)
         self.last_loglik = None   # log-likelihood of the state returned by run()
+        self.launch_events = None  # list -> (start, end) HIP events of each sweep launch
+        self._acc_ws = {}
 
     @staticmethod
     def _resolve(log_target, prior, image_model):
@@ -68,6 +70,16 @@ class SingleComponentMH(object):
         c.locs_max_h, c.locs_max_w = float(hi[0]), float(hi[-1])
         return c
 
+    def _acc_workspace(self, T, dev):
+        """[2T] int32, zeroed once: the kernel leaves it zero after every call
+        (per-tile accept counters + workgroup tickets, smcdet_hip.h)."""
+        key = (T, str(dev))
+        ws = self._acc_ws.get(key)
+        if ws is None:
+            ws = torch.zeros(2 * T, device=dev, dtype=torch.int32)
+            self._acc_ws[key] = ws
+        return ws
+
     def run(self, data, counts, locs, fluxes, temperature, log_target=None, *, prior=None,
             image_model=None, ancestors=None, replay=None, want_loglik=True):
         """kernel.py:26-130.  ancestors [numH,numW,N] (int64, optional) gathers
@@ -96,7 +108,7 @@ class SingleComponentMH(object):
             counts_out = torch.empty_like(counts)
             anc_p = _hip.ptr(ancestors)
         acc = torch.empty(nH, nW, device=dev, dtype=torch.float32)
-        acc_ws = torch.empty(T, device=dev, dtype=torch.int32)
+        acc_ws = self._acc_workspace(T, dev)
         ll = torch.empty(nH, nW, N, device=dev, dtype=torch.float32) if want_loglik else None
         rp = None
         keep = []
@@ -109,12 +121,19 @@ class SingleComponentMH(object):
         off = self.rng.take(self.num_iters)
         cm, cp, ch = image_model._cmodel(), prior._cprior(), self._cmh(prior)
         flags = (_hip.SMCDET_MH_FULL_RECOMPUTE if self.full_recompute else 0) | self.debug_flags
+        ev = self.launch_events
+        if ev is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(torch.cuda.current_stream(dev))
         _hip.check(_hip.lib().smcdet_mh_sweep(
             _hip.ref(cm), _hip.ref(cp), _hip.ref(ch), _hip.ptr(data), _hip.ptr(temperature),
             T, N, S, anc_p, _hip.ptr(counts), _hip.ptr(locs), _hip.ptr(fluxes),
             _hip.ptr(counts_out), _hip.ptr(locs_out), _hip.ptr(fluxes_out), self.rng.seed, off,
             _hip.ref(rp) if rp is not None else None, flags, _hip.ptr(ll), _hip.ptr(acc),
             _hip.ptr(acc_ws), _hip.stream_of(locs)), "smcdet_mh_sweep")
+        if ev is not None:
+            e1.record(torch.cuda.current_stream(dev))
+            ev.append((e0, e1))
         del keep
         self.last_loglik = ll
         self.last_counts = counts_out if counts_out is not None else counts

@@ -135,8 +135,12 @@ class SMCsampler(object):
     def temper(self):
         """sampler.py:99-125, root-finding on device."""
         self.loglik = self._current_loglik()
-        new_t = self.temperature.clone()
-        prev_t = torch.empty_like(new_t)
+        # temperature / log Z are updated in place by the kernel (no per-step
+        # device copies); temperature_prev is a second persistent buffer
+        new_t = self.temperature
+        prev_t = getattr(self, "temperature_prev", None)
+        if prev_t is None or prev_t is new_t or prev_t.shape != new_t.shape:
+            prev_t = torch.empty_like(new_t)
         _hip.check(_hip.lib().smcdet_temper(
             _hip.ptr(self.loglik), _hip.ptr(new_t), _hip.ptr(prev_t), self._T,
             self.loglik.shape[-1], float(self.ess_threshold), _hip.stream_of(new_t)),
@@ -195,20 +199,25 @@ class SMCsampler(object):
             self.tiled_image, self.counts, self.locs, self.fluxes, self.temperature,
             self.log_target, ancestors=ancestors)
         if ancestors is not None:
+            # fused resample: the gather happened inside the sweep.  The uniform
+            # 1/N weights it implies are not materialised: the next
+            # _temper_reweight (which always follows in run()) overwrites them.
             self.counts = self.MutationKernel.last_counts
-            self.weights = torch.full_like(self.weights, 1.0 / self.weights.shape[-1])
         self._fresh_loglik = self.MutationKernel.last_loglik
 
     def _temper_reweight(self, with_resample):
         """temper + update_weights (+ next resampling indices), one launch."""
         self.loglik = self._current_loglik()
         N = self.loglik.shape[-1]
-        new_t = self.temperature.clone()
-        prev_t = torch.empty_like(new_t)
+        # temperature / log Z are updated in place by the kernel (no per-step
+        # device copies); temperature_prev is a second persistent buffer
+        new_t = self.temperature
+        prev_t = getattr(self, "temperature_prev", None)
+        if prev_t is None or prev_t is new_t or prev_t.shape != new_t.shape:
+            prev_t = torch.empty_like(new_t)
         self.weights_log_unnorm = torch.empty_like(self.loglik)
         self.weights = torch.empty_like(self.loglik)
         self.ess = torch.empty_like(new_t)
-        self.log_normalizing_constant = self.log_normalizing_constant.clone()
         idx = None
         off = 0
         if with_resample:

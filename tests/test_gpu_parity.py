@@ -130,10 +130,15 @@ def test_mh_replay_vs_reference(name, full):
     np.testing.assert_allclose(N(l), d["locs1"], rtol=0, atol=2e-5)
     np.testing.assert_allclose(N(f), d["fluxes1"], rtol=2e-6, atol=1e-3)
     np.testing.assert_array_equal(N(acc), d["acc"])
-    # the returned log-likelihood is that of the returned state
+    # the returned log-likelihood is that of the returned state: bit-equal to a
+    # fresh render in full mode; summed over the incrementally maintained rate
+    # image otherwise (float32 update rounding: a few ulp of the total)
     td, model, prior, _ = p_mh_fixture_setup(name)
     ll = model.loglikelihood(T(tiles_of(d["image"], td)), l, f)
-    np.testing.assert_array_equal(N(mh.last_loglik), N(ll))
+    if full:
+        np.testing.assert_array_equal(N(mh.last_loglik), N(ll))
+    else:
+        np.testing.assert_allclose(N(mh.last_loglik), N(ll), rtol=2e-6, atol=1e-3)
 
 
 def test_temper_update_weights_vs_reference():
@@ -182,6 +187,23 @@ def test_systematic_resample_bit_exact():
         W = (w / w.sum(-1, keepdims=True)).astype(np.float32)
         U = rng.random((2, 3)).astype(np.float32)
         np.testing.assert_array_equal(_resample_idx(W, U), O.systematic_resample_index(W, U))
+    # degenerate weights: one-hot, runs of zeros, ties, mass short of 1, U ~ 1
+    for Np in (5, 4096, 8192):
+        cases = []
+        one = np.zeros(Np, np.float32)
+        one[Np // 3] = 1.0
+        cases.append(one)
+        sparse = np.zeros(Np, np.float32)
+        sparse[[0, Np // 2, Np - 1]] = [0.25, 0.5, 0.25]
+        cases.append(sparse)
+        cases.append(np.full(Np, 1.0 / Np, np.float32))          # all ties
+        short = np.full(Np, 0.9 / Np, np.float32)                  # cumsum ends below u
+        cases.append(short)
+        W = np.stack(cases).reshape(1, len(cases), Np)
+        for u in (0.0, 0.5, np.nextafter(np.float32(1), np.float32(0))):
+            U = np.full((1, len(cases)), u, np.float32)
+            np.testing.assert_array_equal(_resample_idx(W, U),
+                                          O.systematic_resample_index(W, U))
 
 
 def test_multinomial_resample_distribution():
@@ -323,5 +345,7 @@ def test_mh_incremental_matches_full_recompute_c2():
             ((outs[0][1] - outs[1][1]).abs().amax(-1) < 1e-3)
     assert float(close.float().mean()) > 0.97, float(close.float().mean())
     ll_ref = model.loglikelihood(img, outs[0][0], outs[0][1])
-    np.testing.assert_array_equal(N(outs[0][3]), N(ll_ref))
+    np.testing.assert_allclose(N(outs[0][3]), N(ll_ref), rtol=2e-6, atol=1e-3)
+    ll_ref_full = model.loglikelihood(img, outs[1][0], outs[1][1])
+    np.testing.assert_array_equal(N(outs[1][3]), N(ll_ref_full))
     assert float(same.float().mean()) > 0.5
