@@ -19,8 +19,14 @@ $(LIB): $(OBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# profiling build with in-kernel phase timestamps (scripts/trace_phases.py)
+TRACE_LIB := smcdet_amd/libsmcdet_hip_trace.so
+trace: $(TRACE_LIB)
+$(TRACE_LIB): $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -DSMCDET_TRACE -shared -o $@ $(SRCS)
+
 clean:
-	rm -f $(OBJS) $(LIB)
+	rm -f $(OBJS) $(LIB) $(TRACE_LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all clean oracle
+.PHONY: all clean oracle trace

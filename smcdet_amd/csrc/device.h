@@ -12,6 +12,67 @@
 namespace smcdet {
 
 constexpr int kWave = 64;
+
+// Phase timestamps for profiling builds only (make trace -> -DSMCDET_TRACE):
+// lane 0 of a traced wave stores s_memtime into a per-file device table that
+// smcdet_trace_read_<file>() copies out.  Compiled out of the product library.
+constexpr int kTraceRows = 256, kTraceCols = 16;
+#ifdef SMCDET_TRACE
+#define SMCDET_TRACE_TABLE static __device__ unsigned long long g_trace[kTraceRows * kTraceCols];
+#define SMC_TRACE(row, col)                                                           \
+  do {                                                                                \
+    const int r_ = (row);                                                             \
+    if (r_ >= 0 && r_ < kTraceRows && (threadIdx.x & 63) == 0)                        \
+      g_trace[r_ * kTraceCols + (col)] = __builtin_amdgcn_s_memtime();                \
+  } while (0)
+// per-wave lifetime record: realtime start/end (100 MHz), memtime start/end, HW_ID
+constexpr int kTraceWaves = 8192;
+#define SMCDET_WAVE_TABLE static __device__ unsigned long long g_wave[kTraceWaves * 8];
+#define SMC_WAVE_MARK(idx, col)                                                       \
+  do {                                                                                \
+    const int i_ = (idx);                                                             \
+    if (i_ >= 0 && i_ < kTraceWaves && (threadIdx.x & 63) == 0) {                     \
+      g_wave[i_ * 8 + (col)] = __builtin_amdgcn_s_memrealtime();                      \
+      g_wave[i_ * 8 + 2 + (col)] = __builtin_amdgcn_s_memtime();                      \
+      if ((col) == 0) {                                                               \
+        g_wave[i_ * 8 + 4] = __builtin_amdgcn_s_getreg(0xF804);                      \
+        g_wave[i_ * 8 + 7] = __builtin_amdgcn_s_getreg(0x7814);                      \
+      }                                                                               \
+    }                                                                                 \
+  } while (0)
+#define SMC_WAVE_STAT(idx, col, v)                                                    \
+  do {                                                                                \
+    const int i_ = (idx);                                                             \
+    if (i_ >= 0 && i_ < kTraceWaves && (threadIdx.x & 63) == 0)                       \
+      g_wave[i_ * 8 + (col)] = (unsigned long long)(v);                               \
+  } while (0)
+#define SMCDET_WAVE_READER(name)                                                      \
+  extern "C" int name(unsigned long long* host, int n) {                             \
+    if (n > kTraceWaves * 8) n = kTraceWaves * 8;                                     \
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave), n * sizeof(unsigned long long)) \
+                   == hipSuccess ? 0 : -3;                                            \
+  }
+#define SMCDET_TRACE_READER(name)                                                     \
+  extern "C" int name(unsigned long long* host, int n) {                             \
+    if (n > kTraceRows * kTraceCols) n = kTraceRows * kTraceCols;                     \
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace), n * sizeof(unsigned long long)) \
+                   == hipSuccess ? 0 : -3;                                            \
+  }
+#else
+#define SMCDET_TRACE_TABLE
+#define SMCDET_WAVE_TABLE
+#define SMC_WAVE_MARK(idx, col) \
+  do {                          \
+  } while (0)
+#define SMC_WAVE_STAT(idx, col, v) \
+  do {                             \
+  } while (0)
+#define SMCDET_WAVE_READER(name)
+#define SMC_TRACE(row, col) \
+  do {                      \
+  } while (0)
+#define SMCDET_TRACE_READER(name)
+#endif
 constexpr float kHalfLog2Pi = 0.91893853320467274178f;  // 0.5*log(2*pi)
 constexpr float kLn2 = 0.69314718055994530942f;
 constexpr float kLog2e = 1.44269504088896340736f;

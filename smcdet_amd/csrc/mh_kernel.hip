@@ -36,6 +36,9 @@
 
 namespace smcdet {
 
+SMCDET_TRACE_TABLE
+SMCDET_WAVE_TABLE
+
 constexpr int kMhWaves = 4;
 constexpr int kMhBlock = kMhWaves * kWave;
 constexpr int kSlots = 6;  // register-resident window passes (6*64 = 384 positions)
@@ -151,6 +154,9 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   extern __shared__ float smem[];
   __shared__ int wg_acc, wg_done;  // last-iteration accepts / finished waves of this workgroup
   const DevModel& m = a.m;
+  [[maybe_unused]] const int trow = (int)(blockIdx.x * kMhWaves + (threadIdx.x >> 6));
+  SMC_TRACE(trow, 0);
+  SMC_WAVE_MARK(trow, 0);
   const int HW = m.H * m.W;
   const int HWp = HW + kWave;  // + one dummy cell per lane (HW + lane) for masked lanes
   const int t = blockIdx.y;
@@ -170,6 +176,7 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
     if (MODEL == SMCDET_MODEL_POISSON) lg[HW + threadIdx.x] = 0.f;
   }
   __syncthreads();
+  SMC_TRACE(trow, 1);
   const int n = blockIdx.x * kMhWaves + wave;
   if (n >= a.N) return;
 
@@ -192,6 +199,7 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   tn_cache(sw, a.isl, a.lb_w, a.ub_w, ph_w, lZ_w);
   tn_cache(sfx, a.isf, a.lb_f, a.ub_f, ph_f, lZ_f);
   float lfx = fast_log(sfx);
+  SMC_TRACE(trow, 2);
 
   const float tau = a.temperature[t];
   double cur_ll;
@@ -205,6 +213,7 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
     cur_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
   }
   lam[HW + lane] = m.bg;
+  SMC_TRACE(trow, 3);
 
   // ---- proposals, batched: lane 3b+d proposes dimension d (h, w, flux) of
   // iteration batch_k0 + b (b < kBatch), from the state at batch time.  An
@@ -279,7 +288,24 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   };
 
   int accept = 0;
+#ifdef SMCDET_TRACE
+  unsigned tr_pos = 0, tr_acc = 0;
+#endif
+  // Progress-based issue priority: the SIMD's arbiter otherwise favours the
+  // oldest of its 4 resident waves, which then finish one after another and
+  // leave the SIMD with a single (latency-bound) wave for the last quarter of
+  // the sweep.  Waves ahead of the others drop to a lower priority so the four
+  // progress together and keep the SIMD saturated to the end.
+  int prio_lvl = 0;
+  __builtin_amdgcn_s_setprio(3);
   for (int k = 0; k < a.K; ++k) {
+    const int lvl = (k * 4) / a.K;
+    if (lvl != prio_lvl) {
+      prio_lvl = lvl;
+      if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+      else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
     const int kl = k & 63;
     if (kl == 0) refill(k);
     if (k >= batch_k0 + batch_n) compute_batch(k);
@@ -336,6 +362,9 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
       bw = c1 - c0 + 1;
       npos = (r1 >= r0 && c1 >= c0 && !ablate_lik) ? (r1 - r0 + 1) * bw : 0;
       nslots = (npos + kWave - 1) / kWave;
+#ifdef SMCDET_TRACE
+      tr_pos += npos;
+#endif
       const unsigned magic = (65536u + (unsigned)bw - 1u) / (unsigned)bw;  // q/bw, q < 1024
       const bool same = (fh0 == fh1) && (fw0 == fw1);
       const int ao_h = fh0 - m.R - r0, ao_w = fw0 - m.R - c0;
@@ -351,9 +380,9 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
           const int q = i * kWave + lane;
           const bool valid = q < npos;
           const int aa = (int)(__umul24((unsigned)q, magic) >> 16);
-          const int bb = q - aa * bw;
+          const int bb = q - (int)__umul24((unsigned)aa, (unsigned)bw);
           const int ph = r0 + aa, pw = c0 + bb;
-          const int p = valid ? ph * m.W + pw : HW + lane;
+          const int p = valid ? (int)__umul24((unsigned)ph, (unsigned)m.W) + pw : HW + lane;
           float lnew;
           const float e = position_delta<MODEL, win>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
                                                      amp_n, ao_h, ao_w, an_h, an_w, lnew);
@@ -381,10 +410,10 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
           const float inv_bw = 1.0f / (float)bw;
           for (int q = kSlots * kWave + lane; q < npos; q += kWave) {
             const int aa = (int)(((float)q + 0.5f) * inv_bw);
-            const int bb = q - aa * bw;
+            const int bb = q - (int)__umul24((unsigned)aa, (unsigned)bw);
             const int ph = r0 + aa, pw = c0 + bb;
             float lnew;
-            dsum += position_delta<MODEL, true>(m, xs, lg, lam, ph * m.W + pw, aa, bb, ph, pw,
+            dsum += position_delta<MODEL, true>(m, xs, lg, lam, (int)__umul24((unsigned)ph, (unsigned)m.W) + pw, aa, bb, ph, pw,
                                                 P, amp_o, amp_n, ao_h, ao_w, an_h, an_w, lnew);
           }
         }
@@ -397,6 +426,9 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
     const float e = fast_exp(loga);
     const float alpha = e > 1.0f ? 1.0f : e;  // clamp(max=1) keeps NaN
     accept = __builtin_amdgcn_readfirstlane((uacc <= alpha) ? 1 : 0);
+#ifdef SMCDET_TRACE
+    tr_acc += accept;
+#endif
     if (accept) {
       if constexpr (FULL) {
         cur_ll = new_ll;
@@ -412,12 +444,12 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
           const float inv_bw = 1.0f / (float)bw;
           for (int q = kSlots * kWave + lane; q < npos; q += kWave) {
             const int aa = (int)(((float)q + 0.5f) * inv_bw);
-            const int bb = q - aa * bw;
+            const int bb = q - (int)__umul24((unsigned)aa, (unsigned)bw);
             const int ph = r0 + aa, pw = c0 + bb;
             float lnew;
-            (void)position_delta<MODEL, true>(m, xs, lg, lam, ph * m.W + pw, aa, bb, ph, pw, P,
+            (void)position_delta<MODEL, true>(m, xs, lg, lam, (int)__umul24((unsigned)ph, (unsigned)m.W) + pw, aa, bb, ph, pw, P,
                                               amp_o, amp_n, ao_h, ao_w, an_h, an_w, lnew);
-            lam[ph * m.W + pw] = lnew;
+            lam[(int)__umul24((unsigned)ph, (unsigned)m.W) + pw] = lnew;
           }
         }
         cur_ll += (double)dll;
@@ -441,6 +473,12 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
     }
   }
 
+  __builtin_amdgcn_s_setprio(0);
+  SMC_TRACE(trow, 4);
+#ifdef SMCDET_TRACE
+  SMC_WAVE_STAT(trow, 5, tr_pos);
+  SMC_WAVE_STAT(trow, 6, tr_acc);
+#endif
   // ---- write back --------------------------------------------------------------
   if (lane < S) {
     a.locs_out[(pid * S + lane) * 2 + 0] = sh;
@@ -463,6 +501,8 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
     }
     if (lane == 0) a.loglik_out[pid] = (float)ll;
   }
+  SMC_TRACE(trow, 5);
+  SMC_WAVE_MARK(trow, 1);
   // ---- acceptance rate of the last iteration (kernel.py:130), no extra launch:
   // waves add into LDS; the workgroup's last wave adds the total to the tile's
   // counter and takes a ticket; the tile's last workgroup writes the rate and
@@ -519,6 +559,9 @@ static int launch_mh(const MhArgs& a, bool replay, bool full, dim3 grid, size_t 
 }  // namespace smcdet
 
 using namespace smcdet;
+
+SMCDET_TRACE_READER(smcdet_trace_read_mh)
+SMCDET_WAVE_READER(smcdet_trace_read_waves)
 
 extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_prior_t* prior,
                                const smcdet_mh_t* mh, const float* tiled_image,

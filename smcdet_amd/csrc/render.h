@@ -31,11 +31,11 @@ __device__ __forceinline__ void add_source(const DevModel& m, float* lam, float 
   const float ampn = amp * psf_scale<MODEL>(m);
   for (int q = lane; q < npos; q += kWave) {
     const int aa = (int)(((float)q + 0.5f) * inv_bw);
-    const int bb = q - aa * bw;
+    const int bb = q - (int)__umul24((unsigned)aa, (unsigned)bw);
     const int ph = r0 + aa, pw = c0 + bb;
     const float dh = ((float)ph + 0.5f) - h;
     const float dw = ((float)pw + 0.5f) - w;
-    const int p = ph * m.W + pw;
+    const int p = (int)__umul24((unsigned)ph, (unsigned)m.W) + pw;
     lam[p] += ampn * psf_raw<MODEL>(m, fmaf(dh, dh, dw * dw));
   }
   wave_sync();
@@ -95,7 +95,7 @@ __device__ __forceinline__ void render_regs(const DevModel& m, float (&lamk)[PPL
       if (k >= klo && k <= khi) {
         const int p = k * kWave + lane;
         const int ph = (int)(__umul24((unsigned)p, magic) >> 16);
-        const int pw = p - ph * m.W;
+        const int pw = p - (int)__umul24((unsigned)ph, (unsigned)m.W);
         const float dh = ((float)ph + 0.5f) - h;
         const float dw = ((float)pw + 0.5f) - w;
         const float v = amp * psf_raw<MODEL>(m, fmaf(dh, dh, dw * dw));

@@ -17,6 +17,8 @@
 
 namespace smcdet {
 
+SMCDET_TRACE_TABLE
+
 constexpr int kTB = 512;            // threads per tile workgroup
 constexpr int kTW = kTB / kWave;    // 8 waves (2 per SIMD)
 constexpr int kMaxPer = 32;         // log-likelihoods per thread held in registers
@@ -224,6 +226,8 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
   const int N = a.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
+  [[maybe_unused]] const int trow = threadIdx.x < kWave ? t : -1;
+  SMC_TRACE(trow, 0);
   TileLL<PER> ll;
   if (a.flags & (kDoTemper | kDoWeights)) {
     const float* llg = a.loglik + (size_t)t * N;
@@ -240,14 +244,17 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
     for (int j = 0; j < PER; ++j)
       if (ll.valid(j, N)) lm = fmaxf(lm, ll.l[j]);
     lm = block_max(lm, &red, parity);
+    SMC_TRACE(trow, 1);
     const double thr = a.ess_threshold;
     auto f = [&](double x) { return block_ess_objective(ll, N, lm, x, thr, &red, parity); };
     const double top = 1.0 - (double)tau;
     // sampler.py:113-122: root-find only if ESS at delta = 1 - tau is below threshold
     const double ftop = f(top);
+    SMC_TRACE(trow, 2);
     double delta = top;
     // f(0) = N - thr exactly: every weight is exp(0) = 1
     if (ftop < 0.0) delta = block_brentq(f, 0.0, top, (double)N - thr, ftop);
+    SMC_TRACE(trow, 3);
     const float tnew = tau + (float)delta;  // delta tensor is float32 (sampler.py:105)
     d_new = tnew - tau;
     if (threadIdx.x == 0) {
@@ -293,6 +300,7 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
     }
     double qs = tree_sum(q);
     block_sum2(qs, unused, &red, parity);
+    SMC_TRACE(trow, 4);
     if (threadIdx.x == 0) {
       a.ess[t] = (float)(1.0 / qs);
       a.logZ[t] = (a.logZ[t] + mx) + logf(sf / (float)N);
@@ -322,6 +330,7 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
     parity ^= 1;
     if (lane == 63) red.d[k][wave][0] = incl;
     __syncthreads();
+    SMC_TRACE(trow, 5);
     double base = 0.0;
     for (int i = 0; i < wave; ++i) base += red.d[k][i][0];
     double run = base + incl - part;
@@ -360,6 +369,7 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
       };
       for (int i = threadIdx.x; i <= N; i += kTB) slot[i] = 0;
       __syncthreads();
+      SMC_TRACE(trow, 6);
       if (b0 < b1) {
         int cprev = cnt(buf[b0]);
         for (int i = b0; i < b1; ++i) {
@@ -369,6 +379,7 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
         }
       }
       __syncthreads();
+      SMC_TRACE(trow, 7);
       // prefix max over slot[0..N-1], contiguous chunk per thread
       int pm = 0;
       for (int i = b0; i < b1; ++i) pm = max(pm, slot[i]);
@@ -391,7 +402,9 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
         slot[i] = min(run_m, N - 1);
       }
       __syncthreads();
+      SMC_TRACE(trow, 8);
       for (int n = threadIdx.x; n < N; n += kTB) idxg[n] = (int64_t)slot[n];
+      SMC_TRACE(trow, 9);
     } else {
       // multinomial (sampler.py:127-140): target = u * total, first bin > target
       for (int n = threadIdx.x; n < N; n += kTB) {
@@ -486,6 +499,8 @@ static int launch_tile(const TileArgs& a, hipStream_t st) {
 }  // namespace smcdet
 
 using namespace smcdet;
+
+SMCDET_TRACE_READER(smcdet_trace_read_tile)
 
 extern "C" {
 
