@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 2
+#define SMCDET_ABI_VERSION 3
 
 /* status codes */
 #define SMCDET_OK 0
@@ -148,14 +148,22 @@ int smcdet_prior_sample(const smcdet_prior_t* prior, int32_t T,
  * sampler.py:100-102).  acc_count[2T] is an int32 workspace that must be
  * zero before the first call; every call leaves it zero again (it holds the
  * per-tile accept counters and workgroup tickets only while the kernel runs),
- * so one zeroed buffer serves every call on a stream. */
+ * so one zeroed buffer serves every call on a stream.
+ * rate_in / rate_out [T,N,H*W] (both nullable, ignored with
+ * SMCDET_MH_FULL_RECOMPUTE): persisted per-particle rate images
+ * lambda = B + sum_j g f_j psf_j.  With rate_in the sweep starts from the
+ * image of particle ancestors[t,n] instead of re-rendering all S sources;
+ * rate_out receives the image of the returned state (maintained
+ * incrementally, float32 update rounding).  rate_in must describe *_in
+ * exactly; rate_in != rate_out when ancestors is non-null. */
 int smcdet_mh_sweep(const smcdet_image_model_t* model,
                     const smcdet_prior_t* prior, const smcdet_mh_t* mh,
                     const float* tiled_image, const float* temperature,
                     int32_t T, int32_t N, int32_t S, const int64_t* ancestors,
                     const float* counts_in, const float* locs_in,
                     const float* fluxes_in, float* counts_out,
-                    float* locs_out, float* fluxes_out, uint64_t seed,
+                    float* locs_out, float* fluxes_out, const float* rate_in,
+                    float* rate_out, uint64_t seed,
                     uint64_t offset, const smcdet_mh_replay_t* replay,
                     uint32_t flags, float* loglik_out, float* acc_rate,
                     int32_t* acc_count, void* stream);

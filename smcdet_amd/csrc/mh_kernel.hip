@@ -64,6 +64,8 @@ struct MhArgs {
   float* locs_out;
   float* fluxes_out;
   float* loglik_out;                 // [T,N] or null
+  const float* rate_in;              // [T,N,H*W] persisted rate images or null
+  float* rate_out;                   // [T,N,H*W] or null
   int32_t* acc_count;                // [2T] zeroed workspace: counts, tickets
   float* acc_rate;                   // [T]
   const int32_t* r_comp;             // replay (or null)
@@ -202,12 +204,34 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   SMC_TRACE(trow, 2);
 
   const float tau = a.temperature[t];
-  double cur_ll;
-  if constexpr (PPL > 0) {
+  double cur_ll = 0.0;  // tracked only in FULL mode (incremental mode works on deltas)
+  if constexpr (!FULL) {
+    if (a.rate_in) {
+      // the ancestor's rate image, persisted by the previous sweep: no render
+      const float* rin = a.rate_in + src * (size_t)HW;
+      if ((HW & 3) == 0) {
+        for (int p = 4 * lane; p < HW; p += 4 * kWave) {
+          const float4 v = *reinterpret_cast<const float4*>(rin + p);
+          lam[p] = v.x;
+          lam[p + 1] = v.y;
+          lam[p + 2] = v.z;
+          lam[p + 3] = v.w;
+        }
+      } else {
+        for (int p = lane; p < HW; p += kWave) lam[p] = rin[p];
+      }
+      wave_sync();
+    } else if constexpr (PPL > 0) {
+      float lamk[PPL > 0 ? PPL : 1];
+      render_regs<MODEL, PPL>(m, lamk, sh, sw, sfx, S, lane);
+      store_regs<MODEL, PPL>(m, lam, lamk, lane);
+    } else {
+      render_sources<MODEL>(m, lam, sh, sw, sfx, S, lane);
+    }
+  } else if constexpr (PPL > 0) {
     float lamk[PPL > 0 ? PPL : 1];
     render_regs<MODEL, PPL>(m, lamk, sh, sw, sfx, S, lane);
     cur_ll = pixel_sum_regs<MODEL, PPL>(m, xs, lg, lamk, lane);
-    if constexpr (!FULL) store_regs<MODEL, PPL>(m, lam, lamk, lane);
   } else {
     render_sources<MODEL>(m, lam, sh, sw, sfx, S, lane);
     cur_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
@@ -501,6 +525,18 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
     }
     if (lane == 0) a.loglik_out[pid] = (float)ll;
   }
+  if constexpr (!FULL) {
+    if (a.rate_out) {
+      float* rout = a.rate_out + pid * (size_t)HW;
+      if ((HW & 3) == 0) {
+        for (int p = 4 * lane; p < HW; p += 4 * kWave)
+          *reinterpret_cast<float4*>(rout + p) = make_float4(lam[p], lam[p + 1], lam[p + 2],
+                                                             lam[p + 3]);
+      } else {
+        for (int p = lane; p < HW; p += kWave) rout[p] = lam[p];
+      }
+    }
+  }
   SMC_TRACE(trow, 5);
   SMC_WAVE_MARK(trow, 1);
   // ---- acceptance rate of the last iteration (kernel.py:130), no extra launch:
@@ -568,7 +604,8 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
                                const float* temperature, int32_t T, int32_t N, int32_t S,
                                const int64_t* ancestors, const float* counts_in,
                                const float* locs_in, const float* fluxes_in, float* counts_out,
-                               float* locs_out, float* fluxes_out, uint64_t seed,
+                               float* locs_out, float* fluxes_out, const float* rate_in,
+                               float* rate_out, uint64_t seed,
                                uint64_t offset, const smcdet_mh_replay_t* replay, uint32_t flags,
                                float* loglik_out, float* acc_rate, int32_t* acc_count,
                                void* stream) {
@@ -586,6 +623,8 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
   if (ancestors && (locs_in == locs_out || fluxes_in == fluxes_out ||
                     (counts_out && counts_in == counts_out)))
     return set_error(SMCDET_EINVAL, "ancestor gather needs distinct in/out buffers");
+  if (ancestors && rate_in && rate_in == rate_out)
+    return set_error(SMCDET_EINVAL, "ancestor gather needs distinct rate_in/rate_out buffers");
   if (replay && (!replay->comp || !replay->uloc || !replay->uflux || !replay->uacc))
     return set_error(SMCDET_EINVAL, "incomplete replay buffers");
   if (!(mh->locs_stdev > 0.f) || !(mh->fluxes_stdev > 0.f))
@@ -621,6 +660,8 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
   a.locs_out = locs_out;
   a.fluxes_out = fluxes_out;
   a.loglik_out = loglik_out;
+  a.rate_in = rate_in;
+  a.rate_out = rate_out;
   a.acc_count = acc_count;
   a.acc_rate = acc_rate;
   if (replay) {

@@ -80,11 +80,23 @@ class SingleComponentMH(object):
             self._acc_ws[key] = ws
         return ws
 
+    @staticmethod
+    def _rate_buffer(buf, name, TN, data):
+        if buf is None:
+            return None
+        if buf.numel() != TN * data.shape[-1] * data.shape[-2] or not buf.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous [numH,numW,N,H*W] buffer")
+        return _hip.dev_f32(buf, name)
+
     def run(self, data, counts, locs, fluxes, temperature, log_target=None, *, prior=None,
-            image_model=None, ancestors=None, replay=None, want_loglik=True):
+            image_model=None, ancestors=None, replay=None, want_loglik=True, rate_in=None,
+            rate_out=None):
         """kernel.py:26-130.  ancestors [numH,numW,N] (int64, optional) gathers
         the starting state (a fused resample); replay = dict(comp, uloc, uflux,
-        uacc) replays recorded draws."""
+        uacc) replays recorded draws; rate_in / rate_out [numH,numW,N,H*W]
+        (optional) are persisted per-particle rate images: rate_in must be the
+        images of (locs, fluxes), rate_out receives those of the result
+        (ignored in full_recompute mode)."""
         prior, image_model = self._resolve(log_target, prior, image_model)
         data = _hip.dev_f32(data, "data")
         counts = _hip.dev_f32(counts, "counts")
@@ -128,7 +140,10 @@ class SingleComponentMH(object):
         _hip.check(_hip.lib().smcdet_mh_sweep(
             _hip.ref(cm), _hip.ref(cp), _hip.ref(ch), _hip.ptr(data), _hip.ptr(temperature),
             T, N, S, anc_p, _hip.ptr(counts), _hip.ptr(locs), _hip.ptr(fluxes),
-            _hip.ptr(counts_out), _hip.ptr(locs_out), _hip.ptr(fluxes_out), self.rng.seed, off,
+            _hip.ptr(counts_out), _hip.ptr(locs_out), _hip.ptr(fluxes_out),
+            _hip.ptr(self._rate_buffer(rate_in, "rate_in", T * N, data)),
+            _hip.ptr(self._rate_buffer(rate_out, "rate_out", T * N, data)),
+            self.rng.seed, off,
             _hip.ref(rp) if rp is not None else None, flags, _hip.ptr(ll), _hip.ptr(acc),
             _hip.ptr(acc_ws), _hip.stream_of(locs)), "smcdet_mh_sweep")
         if ev is not None:

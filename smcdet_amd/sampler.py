@@ -32,7 +32,8 @@ from ._rng import PhiloxStream
 class SMCsampler(object):
     def __init__(self, image, tile_dim, Prior, ImageModel, MutationKernel, num_catalogs,
                  ess_threshold_prop, resample_method, flux_detection_threshold, max_smc_iters,
-                 print_every=5, *, seed=None, device=None, fused=True):
+                 print_every=5, *, seed=None, device=None, fused=True, persist_rate_images=True,
+                 rate_refresh_every=8):
         if device is None:
             device = image.device if image.is_cuda else torch.device(
                 "cuda", torch.cuda.current_device())
@@ -69,6 +70,17 @@ class SMCsampler(object):
         self.rng = PhiloxStream(seed)
         self.MutationKernel.rng = self.rng
         self.fused = fused
+        # Per-particle rate images kept on device between MH sweeps (double
+        # buffered, [numH,numW,N,H*W] each): a sweep then starts from its
+        # ancestor's image instead of re-rendering all sources.  Every
+        # `rate_refresh_every`-th sweep re-renders from the state, bounding the
+        # float32 drift of the incrementally maintained images.
+        self.persist_rate_images = persist_rate_images
+        self.rate_refresh_every = max(1, int(rate_refresh_every))
+        self._rate = [None, None]
+        self._rate_cur = 0
+        self._rate_valid = False
+        self._rate_age = 0
         self._fresh_loglik = None   # loglik of the current state, if already known
         self._pending_idx = None    # resampling indices computed by the fused tile launch
 
@@ -103,6 +115,7 @@ class SMCsampler(object):
         self.counts, self.locs, self.fluxes = self.Prior.sample_stratified(
             nH, self.num_catalogs, device=self.device, rng=self.rng, tiles_shape=self.tiles_shape)
         self.Prior.num = self.counts.shape[-1]
+        self._rate_valid = False
         self.temperature_prev = self._zeros_tiles()
         self.temperature = self._zeros_tiles()
         self.loglik = self.ImageModel.loglikelihood(self.tiled_image, self.locs, self.fluxes)
@@ -186,6 +199,7 @@ class SMCsampler(object):
         self.counts, self.locs, self.fluxes = c, l, f
         self.weights = torch.full_like(self.weights, 1.0 / N)
         self._fresh_loglik = None
+        self._rate_valid = False  # persisted rate images describe the pre-gather state
 
     def resample(self):
         """sampler.py:127-169."""
@@ -193,11 +207,30 @@ class SMCsampler(object):
         self._pending_idx = None
         self._gather(idx)
 
+    def _rate_buffers(self):
+        """(rate_in, rate_out) for the next sweep, or (None, None)."""
+        if not self.persist_rate_images or getattr(self.MutationKernel, "full_recompute", False):
+            return None, None
+        shape = (*self.locs.shape[:3], self.tile_dim * self.tile_dim)
+        for i in (0, 1):
+            if self._rate[i] is None or tuple(self._rate[i].shape) != shape:
+                self._rate[i] = torch.empty(shape, device=self.device, dtype=torch.float32)
+                self._rate_valid = False
+        fresh = (not self._rate_valid) or self._rate_age + 1 >= self.rate_refresh_every
+        rin = None if fresh else self._rate[self._rate_cur]
+        return rin, self._rate[1 - self._rate_cur]
+
     def mutate(self, ancestors=None):
         """sampler.py:171-179."""
+        rin, rout = self._rate_buffers()
+        kw = {} if rout is None else {"rate_in": rin, "rate_out": rout}
         self.locs, self.fluxes, self.mutation_acc_rates = self.MutationKernel.run(
             self.tiled_image, self.counts, self.locs, self.fluxes, self.temperature,
-            self.log_target, ancestors=ancestors)
+            self.log_target, ancestors=ancestors, **kw)
+        if rout is not None:
+            self._rate_cur = 1 - self._rate_cur
+            self._rate_age = 0 if rin is None else self._rate_age + 1
+            self._rate_valid = True
         if ancestors is not None:
             # fused resample: the gather happened inside the sweep.  The uniform
             # 1/N weights it implies are not materialised: the next

@@ -349,3 +349,39 @@ def test_mh_incremental_matches_full_recompute_c2():
     ll_ref_full = model.loglikelihood(img, outs[1][0], outs[1][1])
     np.testing.assert_array_equal(N(outs[1][3]), N(ll_ref_full))
     assert float(same.float().mean()) > 0.5
+
+
+def test_mh_persisted_rate_images_c2():
+    """Sweeps that start from the ancestor's persisted rate image (no
+    re-render) make the same moves as sweeps that re-render, and the persisted
+    image tracks a fresh render of the state to float32 update rounding."""
+    from smcdet_amd._rng import PhiloxStream
+    torch.manual_seed(12)
+    H, S, Np, K = 32, 10, 1024, 40
+    model, prior = p_m71_model(H), p_m71_prior(H, S, S, counts_rate=0.003125)
+    truth = p_m71_prior(H, 0, 100, counts_rate=0.003125)
+    c, l, f = truth.sample(num_catalogs=1, device=DEV)
+    img = model.sample(l, f)[:, :, :, :, 0].contiguous()
+    counts, locs, fluxes = prior.sample(num_tiles_per_side=1, stratify_by_count=True,
+                                        num_catalogs_per_count=Np, device=DEV)
+    tau = torch.tensor([[0.3]], device=DEV)
+    anc = torch.randint(0, Np, (1, 1, Np), device=DEV, dtype=torch.int64)
+    rates = [torch.empty(1, 1, Np, H * H, device=DEV) for _ in range(2)]
+    res = []
+    for persist in (True, False):
+        mh = p_m71_mh(K)
+        mh.rng = PhiloxStream(5)
+        l1, f1, _ = mh.run(img, counts, locs, fluxes, tau, prior=prior, image_model=model,
+                           rate_out=rates[0] if persist else None)
+        c1 = counts
+        kw = dict(rate_in=rates[0], rate_out=rates[1]) if persist else {}
+        l2, f2, _ = mh.run(img, c1, l1, f1, tau, prior=prior, image_model=model,
+                           ancestors=anc, **kw)
+        res.append((l2, f2, mh.last_loglik))
+    same = ((res[0][0] == res[1][0]).all(-1).all(-1) & (res[0][1] == res[1][1]).all(-1))
+    assert float(same.float().mean()) > 0.99, float(same.float().mean())
+    np.testing.assert_allclose(N(res[0][2]), N(res[1][2]), rtol=2e-6, atol=1e-3)
+    # persisted image of the final state vs a fresh render
+    fresh = model.rate(res[0][0], res[0][1])  # [1,1,H,W,N]
+    fresh = fresh.permute(0, 1, 4, 2, 3).reshape(1, 1, Np, H * H)
+    np.testing.assert_allclose(N(rates[1]), N(fresh), rtol=2e-6, atol=2e-4)

@@ -29,7 +29,7 @@ def _load(which):
         return json.load(f)
 
 
-def _run(which, cfg, image, seed, fused=True):
+def _run(which, cfg, image, seed, fused=True, persist=True):
     from smcdet_amd.sampler import SMCsampler
     torch.manual_seed(seed)
     H, N, S = cfg["tile"], cfg["N"], cfg["S"]
@@ -38,7 +38,8 @@ def _run(which, cfg, image, seed, fused=True):
     else:
         prior, model, mh = p_m71_prior(H, S, S), p_m71_model(H), p_m71_mh(cfg["K"])
     s = SMCsampler(image, H, prior, model, mh, N, cfg["rho"], cfg["method"],
-                   M71["flux_detection_threshold"], 100, print_every=10 ** 9, fused=fused)
+                   M71["flux_detection_threshold"], 100, print_every=10 ** 9, fused=fused,
+                   persist_rate_images=persist)
     esses = []
     orig = s._temper_reweight
 
@@ -108,11 +109,14 @@ def test_statistical_parity_vs_reference(which):
 def test_fused_run_equals_method_by_method_run():
     """run() with the fused schedule (MH gathers the ancestors; one per-tile
     launch does temper + reweight + next resampling indices) consumes the
-    random streams in the same order as the method-by-method schedule."""
+    random streams in the same order as the method-by-method schedule.  (With
+    persisted rate images the fused run starts sweeps from incrementally
+    maintained images, which can flip float32 near-tie decisions: that mode is
+    checked by test_mh_persisted_rate_images_c2 and the statistical tests.)"""
     ref = _load("basic")
     cfg = ref["config"]
     image = torch.tensor(ref["image"], dtype=torch.float32, device="cuda")
-    a = _run("basic", cfg, image, 7, fused=True)
+    a = _run("basic", cfg, image, 7, fused=True, persist=False)
     b = _run("basic", cfg, image, 7, fused=False)
     assert a["iters"] == b["iters"]
     assert a["logZ"] == b["logZ"]
