@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 3
+#define SMCDET_ABI_VERSION 4
 
 /* status codes */
 #define SMCDET_OK 0
@@ -49,6 +49,11 @@ extern "C" {
 
 /* mh flags */
 #define SMCDET_MH_FULL_RECOMPUTE 1u /* re-render every source per step (reference arithmetic) */
+/* draw the moved component from 0..count-1 instead of 0..S-1: a particle of
+ * count s padded to S sources then moves exactly as the reference's
+ * fixed-count kernel with S = s (kernel.py:35-37); count 0 never moves.
+ * Used by the count-stratified sampler (CS-SMC). */
+#define SMCDET_MH_COMPONENT_BY_COUNT 2u
 /* diagnostic ablations (timing only; results are NOT valid samples) */
 #define SMCDET_MH_ABLATE_LIKELIHOOD 256u /* skip the delta-likelihood passes */
 #define SMCDET_MH_ABLATE_PROPOSAL 512u   /* skip the truncated-normal proposal math */
@@ -205,6 +210,28 @@ int smcdet_gather(const int64_t* idx, int32_t T, int32_t N, int32_t S,
                   const float* counts_in, const float* locs_in,
                   const float* fluxes_in, float* counts_out, float* locs_out,
                   float* fluxes_out, void* stream);
+
+/* Count-stratified SMC combination (manuscript/manuscript.tex:344-354,
+ * Algorithm 2; the reference describes CS-SMC but has no code for it at HEAD).
+ * Per image tile t, with NS count strata k (count s_min + k) whose fixed-count
+ * samplers ran as "stratum tiles" t*NS + k of N equally weighted particles:
+ *   probs[t,k] = p(s|x) = softmax_k(log_norm_const[t*NS+k] + log_count_prior[k])
+ *   then n_out catalogs: stratum k_n ~ probs[t,:] (systematic: u_n = (n+U)/n_out,
+ *   first k with cumsum(probs) >= u_n; multinomial: iid u_n), and a uniform
+ *   particle m_n = floor(v_n * N) of that stratum; idx[t,n] = k_n*N + m_n and
+ *   the catalog (counts [T,NS,N], locs [T,NS,N,S,2], fluxes [T,NS,N,S]) is
+ *   gathered to counts_out [T,n_out], locs_out, fluxes_out.
+ * u_strata ([T] systematic / [T,n_out] multinomial) and u_pick [T,n_out]
+ * replay the uniforms when non-null. */
+int smcdet_count_posterior(const float* log_norm_const,
+                           const float* log_count_prior, int32_t T, int32_t NS,
+                           int32_t N, int32_t S, int32_t n_out,
+                           int32_t resample_method, uint64_t seed,
+                           uint64_t offset, const float* u_strata,
+                           const float* u_pick, const float* counts_in,
+                           const float* locs_in, const float* fluxes_in,
+                           float* probs, int64_t* idx, float* counts_out,
+                           float* locs_out, float* fluxes_out, void* stream);
 
 /* SMCsampler.prune (smcdet/sampler.py:198-219): counts_out[T,N] int64,
  * kept sources compacted to the front in their original order. */

@@ -575,3 +575,49 @@ def smc_run_replay(image, tile_dim, prior, model, mh, num_catalogs, draws,
                 logZ=logZ, temperature=tau, iters=it, acc=acc, pruned_counts=pc,
                 pruned_locs=pl, pruned_fluxes=pf,
                 trace={k: np.stack(v) for k, v in trace.items()})
+
+
+# ---------------------------------------------------------------------------
+# count-stratified SMC combination (manuscript/manuscript.tex:344-354)
+# ---------------------------------------------------------------------------
+def log_count_prior(prior, dtype=np.float64):
+    """log p(s), s = min..max: Poisson(mu).log_prob (prior.py:91-97) for the
+    M71 prior, DiscreteUniform(min, max).log_prob (distributions.py:14-19)
+    otherwise."""
+    s = np.arange(prior.min_objects, prior.max_objects + 1, dtype=dtype)
+    if isinstance(prior, M71PriorP):
+        mu = dtype(prior.poisson_mean())
+        return s * np.log(mu) - mu - gammaln(s + 1)
+    return np.full(s.shape, -np.log(s.size), dtype=dtype)
+
+
+def count_posterior(log_Z, log_prior_s):
+    """p(s|x) = p(s) Z_s / sum_s' p(s') Z_s' (manuscript.tex:344) over the last
+    axis of log_Z [..., NS]; float64."""
+    v = np.asarray(log_Z, np.float64) + np.asarray(log_prior_s, np.float64)
+    m = v.max(-1, keepdims=True)
+    e = np.exp(v - m)
+    return e / e.sum(-1, keepdims=True)
+
+
+def count_posterior_draw(probs, u_strata, u_pick, N, method="systematic"):
+    """s^n ~ p(s|x) and a uniform particle of that stratum (manuscript.tex:349).
+    probs [T, NS] (float64), u_strata [T] (systematic) or [T, n_out]
+    (multinomial), u_pick [T, n_out] float32.  Stratum of draw n = first k with
+    cumsum(probs)[k] >= u_n (u_n = (n + U)/n_out for systematic), particle
+    m_n = min(floor(v_n * N), N - 1) in float32.  Returns flat indices
+    k_n * N + m_n [T, n_out]."""
+    probs = np.asarray(probs, np.float64)
+    T, NS = probs.shape
+    u_pick = np.asarray(u_pick, np.float32)
+    n_out = u_pick.shape[-1]
+    cdf = np.cumsum(probs, -1)
+    if method == "systematic":
+        u = (np.arange(n_out)[None] + np.asarray(u_strata, np.float64)[:, None]) / n_out
+    else:
+        u = np.asarray(u_strata, np.float32).astype(np.float64)
+    k = np.empty((T, n_out), np.int64)
+    for t in range(T):
+        k[t] = np.minimum(np.searchsorted(cdf[t], u[t], side="left"), NS - 1)
+    m = np.minimum((u_pick * np.float32(N)).astype(np.int64), N - 1)
+    return k * N + m

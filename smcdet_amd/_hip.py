@@ -21,6 +21,7 @@ SMCDET_PRIOR_PARETO = 2
 SMCDET_RESAMPLE_MULTINOMIAL = 0
 SMCDET_RESAMPLE_SYSTEMATIC = 1
 SMCDET_MH_FULL_RECOMPUTE = 1
+SMCDET_MH_COMPONENT_BY_COUNT = 2
 
 c_f = ctypes.c_float
 c_i = ctypes.c_int32
@@ -71,6 +72,8 @@ _SIGS = {
     "smcdet_temper_reweight": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_d, c_i, c_u64,
                                 c_u64, c_p, c_p], c_i),
     "smcdet_gather": ([c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
+    "smcdet_count_posterior": ([c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_u64, c_u64, c_p, c_p,
+                                c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
     "smcdet_prune": ([c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p, c_p, c_p, c_p], c_i),
 }
 EXPORTS = tuple(_SIGS)

@@ -125,6 +125,7 @@ enum RngTag : uint32_t {
   kTagPriorFlux = 0x50520001u,
   kTagResample = 0x52530000u,
   kTagNoise = 0x4e530000u,
+  kTagStrata = 0x43530000u,
 };
 
 // ---------------------------------------------------------------------------

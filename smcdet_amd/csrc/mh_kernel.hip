@@ -54,6 +54,7 @@ struct MhArgs {
   uint32_t k0, k1;                   // Philox key (seed)
   uint64_t offset;                   // Philox counter base (iterations)
   uint32_t ablate;                   // SMCDET_MH_ABLATE_* (diagnostics)
+  int by_count;                      // SMCDET_MH_COMPONENT_BY_COUNT
   const float* img;                  // [T,H,W]
   const float* temperature;          // [T]
   const int64_t* ancestors;          // [T,N] or null
@@ -187,6 +188,10 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   const size_t src = a.ancestors ? (size_t)t * N + (size_t)a.ancestors[pid] : pid;
   const float count = a.counts_in[src];
   if (a.counts_out && lane == 0) a.counts_out[pid] = count;
+  // range of the moved component: 0..S-1 (kernel.py:35-37), or 0..count-1
+  // for count-stratified populations padded to S sources (count 0: no moves)
+  const int Sj = a.by_count ? min(max((int)count, 0), S) : S;
+  const int K = Sj > 0 ? a.K : 0;
 
   // ---- particle state: lane s holds source s --------------------------------
   float sh = 0.f, sw = 0.f, sfx = 0.f;
@@ -284,12 +289,12 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   int bj = 0, batch_k0 = 0, batch_n = 0;
   uint64_t dirty = 0;
   auto compute_batch = [&](int k0) {
-    const int n_ = min(min(kBatch, kWave - (k0 & 63)), a.K - k0);
+    const int n_ = min(min(kBatch, kWave - (k0 & 63)), K - k0);
     const int b = min(lb3, n_ - 1);
     const int kl = (k0 & 63) + b;
     int j;
     if constexpr (REPLAY) j = __shfl(rcomp, kl, kWave);
-    else j = min((int)(__shfl(ru0, kl, kWave) * (float)S), S - 1);
+    else j = min((int)(__shfl(ru0, kl, kWave) * (float)Sj), Sj - 1);
     const float u1 = __shfl(ru1, kl, kWave), u2 = __shfl(ru2, kl, kWave);
     const float u3 = __shfl(ru3, kl, kWave);
     const float u = d == 0 ? u1 : (d == 1 ? u2 : u3);
@@ -322,8 +327,8 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   // progress together and keep the SIMD saturated to the end.
   int prio_lvl = 0;
   __builtin_amdgcn_s_setprio(3);
-  for (int k = 0; k < a.K; ++k) {
-    const int lvl = (k * 4) / a.K;
+  for (int k = 0; k < K; ++k) {
+    const int lvl = (k * 4) / K;
     if (lvl != prio_lvl) {
       prio_lvl = lvl;
       if (lvl == 1) __builtin_amdgcn_s_setprio(2);
@@ -678,6 +683,7 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
   const dim3 grid((N + kMhWaves - 1) / kMhWaves, T);
   const bool full = (flags & SMCDET_MH_FULL_RECOMPUTE) != 0;
   a.ablate = flags & (SMCDET_MH_ABLATE_LIKELIHOOD | SMCDET_MH_ABLATE_PROPOSAL);
+  a.by_count = (flags & SMCDET_MH_COMPONENT_BY_COUNT) != 0;
   rc = a.m.model == SMCDET_MODEL_M71
            ? launch_mh<SMCDET_MODEL_M71>(a, replay != nullptr, full, grid, lds, st)
            : launch_mh<SMCDET_MODEL_POISSON>(a, replay != nullptr, full, grid, lds, st);

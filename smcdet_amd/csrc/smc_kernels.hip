@@ -476,6 +476,87 @@ __global__ void prune_kernel(const float* __restrict__ locs, const float* __rest
   }
 }
 
+// ---------------------------------------------------------------------------
+// CS-SMC combination (manuscript.tex:344-354): one workgroup per image tile.
+// p(s|x) in double from the strata's log evidences and the count prior; the
+// stratum of output catalog n by inverse CDF (same float64 arithmetic as the
+// oracle, oracle/smc_oracle.py count_posterior_draw), then a uniform particle
+// of that stratum, gathered straight to the output.
+// ---------------------------------------------------------------------------
+constexpr int kMaxStrata = 1024;
+
+struct CountPostArgs {
+  int T, NS, N, S, n_out, method;
+  uint32_t k0, k1;
+  uint64_t offset;
+  const float* logZ;
+  const float* lcp;
+  const float* u_strata;
+  const float* u_pick;
+  const float* cin;
+  const float* lin;
+  const float* fin;
+  float* probs;
+  int64_t* idx;
+  float* cout;
+  float* lout;
+  float* fout;
+};
+
+__global__ __launch_bounds__(256) void count_posterior_kernel(CountPostArgs a) {
+  __shared__ double cdf[kMaxStrata];
+  __shared__ double U;
+  const int t = blockIdx.x;
+  const int NS = a.NS;
+  if (threadIdx.x == 0) {
+    double m = -INFINITY;
+    for (int k = 0; k < NS; ++k)
+      m = fmax(m, (double)a.logZ[(size_t)t * NS + k] + (double)a.lcp[k]);
+    double s = 0.0;
+    for (int k = 0; k < NS; ++k) s += exp((double)a.logZ[(size_t)t * NS + k] + (double)a.lcp[k] - m);
+    double c = 0.0;
+    for (int k = 0; k < NS; ++k) {
+      const double p = exp((double)a.logZ[(size_t)t * NS + k] + (double)a.lcp[k] - m) / s;
+      a.probs[(size_t)t * NS + k] = (float)p;
+      c += p;
+      cdf[k] = c;
+    }
+    if (a.method == SMCDET_RESAMPLE_SYSTEMATIC) {
+      if (a.u_strata) {
+        U = (double)a.u_strata[t];
+      } else {
+        const U4 r = philox4x32((uint32_t)a.offset, (uint32_t)(a.offset >> 32), (uint32_t)t,
+                                kTagStrata, a.k0, a.k1);
+        U = (double)u01(r.y);
+      }
+    }
+  }
+  __syncthreads();
+  const int N = a.N, S = a.S;
+  for (int n = threadIdx.x; n < a.n_out; n += blockDim.x) {
+    const size_t on = (size_t)t * a.n_out + n;
+    const uint64_t c = a.offset + (uint64_t)n;
+    U4 r{0u, 0u, 0u, 0u};
+    if (!a.u_strata || !a.u_pick)
+      r = philox4x32((uint32_t)c, (uint32_t)(c >> 32), (uint32_t)t, kTagStrata + 1, a.k0, a.k1);
+    double u;
+    if (a.method == SMCDET_RESAMPLE_SYSTEMATIC) u = ((double)n + U) / (double)a.n_out;
+    else u = a.u_strata ? (double)a.u_strata[on] : (double)u01(r.x);
+    int k = 0;
+    while (k < NS - 1 && cdf[k] < u) ++k;
+    const float v = a.u_pick ? a.u_pick[on] : u01(r.y);
+    const int m = min((int)(v * (float)N), N - 1);
+    a.idx[on] = (int64_t)k * N + m;
+    const size_t src = ((size_t)t * NS + k) * N + m;
+    a.cout[on] = a.cin[src];
+    for (int s = 0; s < S; ++s) {
+      a.lout[(on * S + s) * 2 + 0] = a.lin[(src * S + s) * 2 + 0];
+      a.lout[(on * S + s) * 2 + 1] = a.lin[(src * S + s) * 2 + 1];
+      a.fout[on * S + s] = a.fin[src * S + s];
+    }
+  }
+}
+
 static int launch_tile(const TileArgs& a, hipStream_t st) {
   if (a.N > kMaxN)
     return set_error(SMCDET_EUNSUPPORTED, "N=%d particles per tile > %d", a.N, kMaxN);
@@ -608,6 +689,49 @@ int smcdet_gather(const int64_t* idx, int32_t T, int32_t N, int32_t S, const flo
                      (hipStream_t)stream, idx, T, N, S, counts_in, locs_in, fluxes_in, counts_out,
                      locs_out, fluxes_out);
   return check_launch("smcdet_gather");
+}
+
+int smcdet_count_posterior(const float* log_norm_const, const float* log_count_prior, int32_t T,
+                           int32_t NS, int32_t N, int32_t S, int32_t n_out,
+                           int32_t resample_method, uint64_t seed, uint64_t offset,
+                           const float* u_strata, const float* u_pick, const float* counts_in,
+                           const float* locs_in, const float* fluxes_in, float* probs,
+                           int64_t* idx, float* counts_out, float* locs_out, float* fluxes_out,
+                           void* stream) {
+  if (!log_norm_const || !log_count_prior || !counts_in || !probs || !idx || !counts_out ||
+      (S > 0 && (!locs_in || !fluxes_in || !locs_out || !fluxes_out)))
+    return set_error(SMCDET_EINVAL, "null buffer");
+  if (T <= 0 || T > 65535 || N <= 0 || n_out <= 0 || S < 0 || NS <= 0 || NS > kMaxStrata)
+    return set_error(SMCDET_EUNSUPPORTED, "T=%d NS=%d N=%d S=%d n_out=%d", T, NS, N, S, n_out);
+  if (resample_method != SMCDET_RESAMPLE_MULTINOMIAL &&
+      resample_method != SMCDET_RESAMPLE_SYSTEMATIC)
+    return set_error(SMCDET_EINVAL, "unknown resample method %d", resample_method);
+  if ((u_strata == nullptr) != (u_pick == nullptr))
+    return set_error(SMCDET_EINVAL, "u_strata and u_pick must be given together");
+  CountPostArgs a{};
+  a.T = T;
+  a.NS = NS;
+  a.N = N;
+  a.S = S;
+  a.n_out = n_out;
+  a.method = resample_method;
+  a.k0 = (uint32_t)seed;
+  a.k1 = (uint32_t)(seed >> 32);
+  a.offset = offset;
+  a.logZ = log_norm_const;
+  a.lcp = log_count_prior;
+  a.u_strata = u_strata;
+  a.u_pick = u_pick;
+  a.cin = counts_in;
+  a.lin = locs_in;
+  a.fin = fluxes_in;
+  a.probs = probs;
+  a.idx = idx;
+  a.cout = counts_out;
+  a.lout = locs_out;
+  a.fout = fluxes_out;
+  hipLaunchKernelGGL(count_posterior_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("smcdet_count_posterior");
 }
 
 int smcdet_prune(const float* locs, const float* fluxes, int32_t T, int32_t N, int32_t S,

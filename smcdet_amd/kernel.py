@@ -36,6 +36,9 @@ class SingleComponentMH(object):
         # True: re-render every source at every step (the reference's arithmetic);
         # False: incremental delta log-likelihood over the moved source's windows
         self.full_recompute = full_recompute
+        # True: the moved component is drawn from 0..count-1 (fixed-count
+        # strata padded to S sources, see cssmc.py); False: 0..S-1 (kernel.py:35-37)
+        self.component_by_count = False
         self.rng = None           # PhiloxStream; SMCsampler installs its own
         self.debug_flags = 0      # SMCDET_MH_ABLATE_* timing diagnostics (never for sampling)
         self.last_loglik = None   # log-likelihood of the state returned by run()
@@ -133,6 +136,8 @@ class SingleComponentMH(object):
         off = self.rng.take(self.num_iters)
         cm, cp, ch = image_model._cmodel(), prior._cprior(), self._cmh(prior)
         flags = (_hip.SMCDET_MH_FULL_RECOMPUTE if self.full_recompute else 0) | self.debug_flags
+        if self.component_by_count:
+            flags |= _hip.SMCDET_MH_COMPONENT_BY_COUNT
         ev = self.launch_events
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

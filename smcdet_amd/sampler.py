@@ -109,11 +109,16 @@ class SMCsampler(object):
         return self.rng.take(1 if self.resample_method == "systematic" else N)
 
     # ------------------------------------------------------------ the methods
+    def _initial_particles(self):
+        """Stratified prior draw (prior.py:25-64): [numH,numW,N,...]."""
+        return self.Prior.sample_stratified(self.tiles_shape[0], self.num_catalogs,
+                                            device=self.device, rng=self.rng,
+                                            tiles_shape=self.tiles_shape)
+
     def initialize(self):
         """sampler.py:57-85."""
         nH, nW = self.tiles_shape
-        self.counts, self.locs, self.fluxes = self.Prior.sample_stratified(
-            nH, self.num_catalogs, device=self.device, rng=self.rng, tiles_shape=self.tiles_shape)
+        self.counts, self.locs, self.fluxes = self._initial_particles()
         self.Prior.num = self.counts.shape[-1]
         self._rate_valid = False
         self.temperature_prev = self._zeros_tiles()

@@ -574,6 +574,54 @@ def gen_stats(which, seeds):
     print("wrote", path)
 
 
+def cssmc_truth_image():
+    """8x8 M71 image of two moderate stars (flux 6 and 3 nmgy) for the
+    count-stratified targets."""
+    torch.manual_seed(71)
+    l = torch.tensor([[[[[2.5, 3.2], [5.7, 5.1]]]]])
+    f = torch.tensor([[[[6.0, 3.0]]]])
+    return m71_model(8).sample(l, f)[0, 0, :, :, 0]
+
+
+def gen_cssmc(seeds, smax=4, N=512, K=50):
+    """CS-SMC targets (manuscript.tex:314-356): for each count s, the
+    reference's fixed-count SMCsampler (M71Prior with min = max = s) over many
+    seeds -> log Z_s; log Z_0 = the reference's log-likelihood of the empty
+    catalog (one source of flux 0); log p(s) from the reference prior's own
+    Poisson count prior; p(s|x) from each seed's log Z vector."""
+    import contextlib
+    import io
+    torch.set_num_threads(8)
+    img = cssmc_truth_image()
+    model = m71_model(8)
+    ll0 = float(model.loglikelihood(img.reshape(1, 1, 8, 8), torch.full((1, 1, 1, 1, 2), 4.0),
+                                    torch.zeros(1, 1, 1, 1)).flatten()[0])
+    counts = torch.arange(0, smax + 1, dtype=torch.float32)
+    log_ps = m71_prior(8, 0, smax).count_prior.log_prob(counts).numpy().astype(np.float64)
+    rows = []
+    for seed in seeds:
+        lz = [ll0]
+        iters = [1]
+        for s in range(1, smax + 1):
+            torch.manual_seed(1000 * seed + s)
+            mh = SingleComponentMH(K, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+            smp = sampler_for(img, 8, m71_prior(8, s, s), model, mh, N)
+            with contextlib.redirect_stdout(io.StringIO()):
+                smp.run()
+            lz.append(float(smp.log_normalizing_constant.flatten()[0]))
+            iters.append(int(smp.iter))
+        v = np.array(lz) + log_ps
+        p = np.exp(v - v.max())
+        rows.append(dict(seed=seed, logZ=lz, iters=iters, count_posterior=(p / p.sum()).tolist()))
+        print("cssmc", seed, np.round(lz, 2).tolist(), flush=True)
+    cfg = dict(tile=8, N=N, K=K, smin=0, smax=smax, method="systematic", rho=0.5, pad=4,
+               log_count_prior=log_ps.tolist(), loglik_empty=ll0)
+    path = os.path.join(HERE, "stats_cssmc.json")
+    with open(path, "w") as f:
+        json.dump(dict(config=cfg, image=img.numpy().tolist(), runs=rows), f)
+    print("wrote", path)
+
+
 if __name__ == "__main__":
     torch.set_default_dtype(torch.float32)
     what = sys.argv[1] if len(sys.argv) > 1 else "fixtures"
@@ -585,6 +633,9 @@ if __name__ == "__main__":
         gen_mh()
         gen_smc_steps()
         gen_smc_replay()
+    elif what == "cssmc":
+        n = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+        gen_cssmc(list(range(n)))
     elif what == "stats":
         which = sys.argv[2]
         n = int(sys.argv[3]) if len(sys.argv) > 3 else 20
