@@ -57,6 +57,9 @@ extern "C" {
 /* diagnostic ablations (timing only; results are NOT valid samples) */
 #define SMCDET_MH_ABLATE_LIKELIHOOD 256u /* skip the delta-likelihood passes */
 #define SMCDET_MH_ABLATE_PROPOSAL 512u   /* skip the truncated-normal proposal math */
+/* diagnostic: evaluate the union window one position per lane instead of two
+ * (packed arithmetic); same results up to float32 summation order */
+#define SMCDET_MH_SCALAR_SLOTS 1024u
 
 /* Image model (smcdet/images.py:6-26 ImageModel, :105-145 M71ImageModel). */
 typedef struct smcdet_image_model {

@@ -50,7 +50,8 @@ def main():
                 "no_likelihood": (False, _hip.SMCDET_MH_ABLATE_LIKELIHOOD if hasattr(
                     _hip, "SMCDET_MH_ABLATE_LIKELIHOOD") else 256),
                 "no_proposal": (False, 512),
-                "no_both": (False, 768)}
+                "no_both": (False, 768),
+                "scalar_slots": (False, 1024)}
     if a.full:
         variants["full_recompute"] = (True, 0)
     for kk in (0, 1, 25, 200):

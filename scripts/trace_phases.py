@@ -91,6 +91,23 @@ def main():
     out["corr_life_positions"] = float(np.corrcoef(life, npos)[0, 1])
     out["corr_life_accepts"] = float(np.corrcoef(life, nacc)[0, 1])
     out["life_by_xcc"] = {int(x): float(life[xcc == x].mean()) for x in np.unique(xcc)}
+    # per-SIMD view: do the waves sharing a SIMD finish together, and do the
+    # SIMDs carry equal work?
+    xid = (xcc.astype(np.uint64) & 7).astype(np.int64)
+    sid = (xid * 256 + key.astype(np.int64)) * 4 + simd.astype(np.int64)
+    simd_stats = []
+    for v in np.unique(sid):
+        m = sid == v
+        simd_stats.append((m.sum(), end[m].min(), end[m].max(), npos[m].sum()))
+    st = np.array(simd_stats, dtype=np.float64)
+    out["per_simd"] = {
+        "n_simds": int(len(st)), "waves_per_simd_pctl": np.percentile(st[:, 0], [0, 50, 100]).tolist(),
+        "first_end_us_pctl": np.percentile(st[:, 1], [0, 10, 50, 90, 100]).round(1).tolist(),
+        "last_end_us_pctl": np.percentile(st[:, 2], [0, 10, 50, 90, 100]).round(1).tolist(),
+        "within_simd_spread_us_pctl": np.percentile(st[:, 2] - st[:, 1], [0, 10, 50, 90, 100]).round(1).tolist(),
+        "positions_sum_pctl": np.percentile(st[:, 3], [0, 10, 50, 90, 100]).round(0).tolist(),
+        "corr_last_end_positions": float(np.corrcoef(st[:, 2], st[:, 3])[0, 1]),
+    }
     out["waves"] = {
         "kernel_span_us": float(end.max()), "start_us_pctl": np.percentile(start, [0, 50, 90, 99, 100]).round(1).tolist(),
         "end_us_pctl": np.percentile(end, [0, 10, 50, 90, 100]).round(1).tolist(),

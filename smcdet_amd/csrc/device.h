@@ -305,6 +305,50 @@ __device__ __forceinline__ float pix_delta(const DevModel& m, float x, float lgx
   }
 }
 
+// ---------------------------------------------------------------------------
+// two-wide float vectors: elementwise arithmetic compiles to gfx950's packed
+// v_pk_{fma,mul,add}_f32 (one 6-cycle issue for two lanes' worth of work vs
+// two 4-cycle scalar issues, measured in scripts/probe/isa_probe.hip)
+// ---------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 fma2(f2 a, float b, f2 c) { return fma2(a, f2{b, b}, c); }
+__device__ __forceinline__ f2 fma2(f2 a, float b, float c) { return fma2(a, f2{b, b}, f2{c, c}); }
+__device__ __forceinline__ f2 exp2_2(f2 x) { return f2{fast_exp2(x.x), fast_exp2(x.y)}; }
+__device__ __forceinline__ f2 log2_2(f2 x) { return f2{fast_log2(x.x), fast_log2(x.y)}; }
+__device__ __forceinline__ f2 rcp2(f2 x) { return f2{fast_rcp(x.x), fast_rcp(x.y)}; }
+
+template <int MODEL>
+__device__ __forceinline__ f2 psf_raw2(const DevModel& m, f2 r2) {
+  if constexpr (MODEL == SMCDET_MODEL_M71) {
+    const f2 t1 = exp2_2(m.k1 * r2);
+    const f2 t2 = exp2_2(fma2(r2, m.k2, m.lb2));
+    const f2 t3 = exp2_2(fma2(log2_2(fma2(r2, m.k3, 1.0f)), m.kb, m.lp02));
+    return t1 + t2 + t3;
+  } else {
+    return exp2_2(m.kg * r2);
+  }
+}
+
+template <int MODEL>
+__device__ __forceinline__ f2 pix_delta2(const DevModel& m, f2 x, f2 lgx, f2 lam, f2 dl) {
+  if constexpr (MODEL == SMCDET_MODEL_M71) {
+    const f2 v0 = fma2(lam, m.eta, m.s0sq);
+    const f2 r0 = rcp2(v0);
+    const f2 d0 = x - lam;
+    const f2 a = (m.eta * dl) * r0;
+    const f2 u = 1.0f + a;
+    const f2 ru = rcp2(u);
+    const f2 l1p = fma2(-((u - 1.0f) - a), ru, kLn2 * log2_2(u));  // log1p(a)
+    const f2 q = dl * fma2(m.eta * d0, d0 * r0, fma2(d0, 2.0f, -dl)) * (r0 * ru);
+    return 0.5f * (q - l1p);
+  } else {
+    return f2{pix_delta<MODEL>(m, x.x, lgx.x, lam.x, dl.x),
+              pix_delta<MODEL>(m, x.y, lgx.y, lam.y, dl.y)};
+  }
+}
+
 __device__ __forceinline__ float fast_exp(float x) { return fast_exp2(x * kLog2e); }
 __device__ __forceinline__ float fast_log(float x) { return kLn2 * fast_log2(x); }
 

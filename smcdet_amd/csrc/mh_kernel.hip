@@ -55,6 +55,7 @@ struct MhArgs {
   uint64_t offset;                   // Philox counter base (iterations)
   uint32_t ablate;                   // SMCDET_MH_ABLATE_* (diagnostics)
   int by_count;                      // SMCDET_MH_COMPONENT_BY_COUNT
+  int scalar_slots;                  // SMCDET_MH_SCALAR_SLOTS (diagnostic)
   const float* img;                  // [T,H,W]
   const float* temperature;          // [T]
   const int64_t* ancestors;          // [T,N] or null
@@ -150,9 +151,44 @@ __device__ __forceinline__ float position_delta(const DevModel& m, const float* 
   return pix_delta<MODEL>(m, xs[p], lgx, lo, dl);
 }
 
+// Two positions per lane at once (union-window slots 2i and 2i+1): the float
+// arithmetic runs as packed v_pk_{fma,mul,add}_f32 (one issue for both
+// halves), the transcendentals per half.  Same per-element operation order as
+// position_delta.
+template <int MODEL, bool WINDOWS>
+__device__ __forceinline__ f2 position_delta2(const DevModel& m, const float* xs, const float* lg,
+                                             const float* lam, const int (&p)[2],
+                                             const int (&aa)[2], const int (&bb)[2], f2 fph,
+                                             f2 fpw, const Proposal& P, float amp_o, float amp_n,
+                                             int ao_h, int ao_w, int an_h, int an_w, f2& lnew) {
+  const f2 dho = fph - P.h, dwo = fpw - P.w;
+  const f2 dhn = fph - P.hn, dwn = fpw - P.wn;
+  f2 psi_o = psf_raw2<MODEL>(m, fma2(dho, dho, dwo * dwo));
+  f2 psi_n = psf_raw2<MODEL>(m, fma2(dhn, dhn, dwn * dwn));
+  if (WINDOWS) {
+    const unsigned span = 2u * (unsigned)m.R;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      psi_o[h] = ((unsigned)(aa[h] - ao_h) <= span && (unsigned)(bb[h] - ao_w) <= span) ? psi_o[h]
+                                                                                       : 0.f;
+      psi_n[h] = ((unsigned)(aa[h] - an_h) <= span && (unsigned)(bb[h] - an_w) <= span) ? psi_n[h]
+                                                                                       : 0.f;
+    }
+  }
+  const f2 dl = fma2(psi_n, amp_n, -amp_o * psi_o);
+  const f2 lo = {lam[p[0]], lam[p[1]]};
+  const f2 x = {xs[p[0]], xs[p[1]]};
+  lnew = lo + dl;
+  f2 lgx = {0.f, 0.f};
+  if constexpr (MODEL == SMCDET_MODEL_POISSON) lgx = f2{lg[p[0]], lg[p[1]]};
+  return pix_delta2<MODEL>(m, x, lgx, lo, dl);
+}
+
 // PPL > 0: tiles of <= 64*PPL pixels rendered in registers (render_regs);
 // PPL = 0: LDS render (larger tiles)
-template <int MODEL, bool REPLAY, bool FULL, int PPL>
+// PAIRED: union-window positions two per lane in packed arithmetic (default);
+// false: one per lane (SMCDET_MH_SCALAR_SLOTS, for A/B timing).
+template <int MODEL, bool REPLAY, bool FULL, int PPL, bool PAIRED>
 __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   extern __shared__ float smem[];
   __shared__ int wg_acc, wg_done;  // last-iteration accepts / finished waves of this workgroup
@@ -421,6 +457,62 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
         }
         return acc;
       };
+      // the same, two slots (2i, 2i+1) per lane at once in packed arithmetic
+      // (ODD: one more slot 2*np, one position per lane, as `slots` does)
+      auto pairs = [&](auto NP, auto ODD, auto WIN) -> float {
+        constexpr int np = decltype(NP)::value;
+        constexpr bool odd = decltype(ODD)::value;
+        constexpr bool win = decltype(WIN)::value;
+        f2 acc = {0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < np; ++i) {
+          int aa[2], bb[2], p[2];
+          bool valid[2];
+          f2 fph, fpw;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int q = (2 * i + h) * kWave + lane;
+            valid[h] = q < npos;
+            aa[h] = (int)(__umul24((unsigned)q, magic) >> 16);
+            bb[h] = q - (int)__umul24((unsigned)aa[h], (unsigned)bw);
+            const int ph = r0 + aa[h], pw = c0 + bb[h];
+            p[h] = valid[h] ? (int)__umul24((unsigned)ph, (unsigned)m.W) + pw : HW + lane;
+            fph[h] = (float)ph + 0.5f;
+            fpw[h] = (float)pw + 0.5f;
+          }
+          f2 lnew;
+          f2 e = position_delta2<MODEL, win>(m, xs, lg, lam, p, aa, bb, fph, fpw, P, amp_o, amp_n,
+                                             ao_h, ao_w, an_h, an_w, lnew);
+          e.x = valid[0] ? e.x : 0.f;
+          e.y = valid[1] ? e.y : 0.f;
+          acc += e;
+          s_lam[2 * i] = lnew.x;
+          s_lam[2 * i + 1] = lnew.y;
+          s_pix[2 * i] = p[0];
+          s_pix[2 * i + 1] = p[1];
+        }
+        float acc1 = 0.f;
+        if constexpr (odd) {
+          const int q = 2 * np * kWave + lane;
+          const bool valid = q < npos;
+          const int aa = (int)(__umul24((unsigned)q, magic) >> 16);
+          const int bb = q - (int)__umul24((unsigned)aa, (unsigned)bw);
+          const int ph = r0 + aa, pw = c0 + bb;
+          const int p = valid ? (int)__umul24((unsigned)ph, (unsigned)m.W) + pw : HW + lane;
+          float lnew;
+          const float e = position_delta<MODEL, win>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
+                                                     amp_n, ao_h, ao_w, an_h, an_w, lnew);
+          acc1 = valid ? e : 0.f;
+          s_lam[2 * np] = lnew;
+          s_pix[2 * np] = p;
+        }
+        return (acc.x + acc.y) + acc1;
+      };
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      using One = std::true_type;
+      using Zero = std::false_type;
+      using I2 = std::integral_constant<int, 2>;
       using I3 = std::integral_constant<int, 3>;
       using I5 = std::integral_constant<int, 5>;
       using I8 = std::integral_constant<int, kSlots>;
@@ -428,12 +520,26 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
       using Same = std::false_type;
       float dsum = 0.f;
       if (nslots == 0) {
+      } else if (PAIRED && nslots == 1) {
+        dsum = same ? pairs(I0{}, One{}, Same{}) : pairs(I0{}, One{}, Win{});
+      } else if (PAIRED && nslots == 2) {
+        dsum = same ? pairs(I1{}, Zero{}, Same{}) : pairs(I1{}, Zero{}, Win{});
+      } else if (PAIRED && nslots <= 3) {
+        dsum = same ? pairs(I1{}, One{}, Same{}) : pairs(I1{}, One{}, Win{});
+      } else if (PAIRED && nslots <= 4) {
+        dsum = same ? pairs(I2{}, Zero{}, Same{}) : pairs(I2{}, Zero{}, Win{});
+      } else if (PAIRED && nslots <= 5) {
+        dsum = same ? pairs(I2{}, One{}, Same{}) : pairs(I2{}, One{}, Win{});
+      } else if (PAIRED) {
+        dsum = pairs(I3{}, Zero{}, Win{});
       } else if (nslots <= 3) {
         dsum = same ? slots(I3{}, Same{}) : slots(I3{}, Win{});
       } else if (nslots <= 5) {
         dsum = same ? slots(I5{}, Same{}) : slots(I5{}, Win{});
       } else {
         dsum = slots(I8{}, Win{});
+      }
+      if (nslots > 5) {
         // rare: a union window larger than the register slots (a jump of several px)
         if (npos > kSlots * kWave) {
           const float inv_bw = 1.0f / (float)bw;
@@ -568,11 +674,19 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
 
 template <int MODEL, bool REPLAY, bool FULL, int PPL>
 static int launch_mh1(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
-  const void* fn = (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL>;
+  // FULL mode never evaluates union-window slots: one instantiation
+  constexpr bool kPair = !FULL;
+  const bool paired = kPair && !a.scalar_slots;
+  const void* fn = paired ? (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair>
+                          : (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, false>;
   int rc = ensure_lds(fn, lds);
   if (rc) return rc;
-  hipLaunchKernelGGL((mh_sweep_kernel<MODEL, REPLAY, FULL, PPL>), grid, dim3(kMhBlock), lds, st,
-                     a);
+  if (paired)
+    hipLaunchKernelGGL((mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair>), grid, dim3(kMhBlock),
+                       lds, st, a);
+  else
+    hipLaunchKernelGGL((mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, false>), grid, dim3(kMhBlock),
+                       lds, st, a);
   return SMCDET_OK;
 }
 
@@ -684,6 +798,7 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
   const bool full = (flags & SMCDET_MH_FULL_RECOMPUTE) != 0;
   a.ablate = flags & (SMCDET_MH_ABLATE_LIKELIHOOD | SMCDET_MH_ABLATE_PROPOSAL);
   a.by_count = (flags & SMCDET_MH_COMPONENT_BY_COUNT) != 0;
+  a.scalar_slots = (flags & SMCDET_MH_SCALAR_SLOTS) != 0;
   rc = a.m.model == SMCDET_MODEL_M71
            ? launch_mh<SMCDET_MODEL_M71>(a, replay != nullptr, full, grid, lds, st)
            : launch_mh<SMCDET_MODEL_POISSON>(a, replay != nullptr, full, grid, lds, st);
