@@ -143,6 +143,10 @@ __device__ __forceinline__ float readlane(float v, int lane) {
 __device__ __forceinline__ int readlane(int v, int lane) {
   return __builtin_amdgcn_readlane(v, lane);
 }
+// v with lane `lane` replaced by the wave-uniform x
+__device__ __forceinline__ float writelane(float x, int lane, float v) {
+  return (int)(threadIdx.x & 63) == lane ? x : v;
+}
 
 // 64-lane reductions on DPP (no LDS crossbar round trips): quad_perm
 // [1,0,3,2], [2,3,0,1], row_shr:4, row_shr:8 leave each row's sum in its lane

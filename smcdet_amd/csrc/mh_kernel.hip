@@ -322,6 +322,13 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   };
 
   float bx = 0.f, bph = 0.f, blZ = 0.f, bhd = 0.f, blf = 0.f;
+  // per batch element b, precomputed in its lanes (amortised over the batch
+  // instead of wave-uniform VALU work every iteration): bmu = current value
+  // (lanes 3b+d); bfl = floor(current) | floor(proposed) << 16 (lanes 3b, 3b+1);
+  // lane 3b+2: bampo/bampn = rate amplitudes g f psf_scale of the current /
+  // proposed flux, bdp = prior term, bhs = summed Hastings term
+  float bmu = 0.f, bampo = 0.f, bampn = 0.f, bdp = 0.f, bhs = 0.f;
+  int bfl = 0;
   int bj = 0, batch_k0 = 0, batch_n = 0;
   uint64_t dirty = 0;
   auto compute_batch = [&](int k0) {
@@ -346,6 +353,18 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
       propose_lane<true>(mu, c_ph, c_lZ, u, dm, bx, bph, blZ, bhd, blf);
     else
       propose_lane<false>(mu, c_ph, c_lZ, u, dm, bx, bph, blZ, bhd, blf);
+    bmu = mu;
+    bfl = (int)(((unsigned)ifloor16(mu) & 0xffffu) | ((unsigned)ifloor16(bx) << 16));
+    // lane 3b+2 (flux): amplitudes, prior term (kernel.py:64-112 via
+    // prior.py:220-226: the uniform location terms are constant in the box)
+    // and the Hastings sum of the triple, in the per-iteration order
+    const float lf_cur = __shfl(lfx, j, kWave);
+    bampo = m.g * mu * psf_scale<MODEL>(m);
+    bampn = m.g * bx * psf_scale<MODEL>(m);
+    bdp = ((float)j < count) ? -a.pr.ap1 * (blf - lf_cur) : 0.0f;
+    const float hd0 = __shfl(bhd, max(lane - 2, 0), kWave);
+    const float hd1 = __shfl(bhd, max(lane - 1, 0), kWave);
+    bhs = hd0 + hd1 + bhd;
     bj = j;
     batch_k0 = k0;
     batch_n = n_;
@@ -382,22 +401,18 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
       j = readlane(bj, 0);
     }
     const float uacc = readlane(ru4, kl);
+    // the batch entry is current (its source was not moved since the batch)
     Proposal P;
     P.j = j;
-    P.h = readlane(sh, j);
-    P.w = readlane(sw, j);
-    P.f = readlane(sfx, j);
-    P.lf = readlane(lfx, j);
+    P.h = readlane(bmu, 3 * b);
+    P.w = readlane(bmu, 3 * b + 1);
     P.hn = readlane(bx, 3 * b);
     P.wn = readlane(bx, 3 * b + 1);
     P.fn = readlane(bx, 3 * b + 2);
-    P.hast = readlane(bhd, 3 * b) + readlane(bhd, 3 * b + 1) + readlane(bhd, 3 * b + 2);
-    P.lfn = readlane(blf, 3 * b + 2);
-
-    // prior: uniform locations are constant in the box; flux density term
-    const float dprior = ((float)P.j < count) ? -a.pr.ap1 * (P.lfn - P.lf) : 0.0f;
+    P.hast = readlane(bhs, 3 * b + 2);
+    const float dprior = readlane(bdp, 3 * b + 2);
     // rate contributions g*f*psf, the psf normalisation folded into the amplitude
-    const float amp_o = m.g * P.f * psf_scale<MODEL>(m), amp_n = m.g * P.fn * psf_scale<MODEL>(m);
+    const float amp_o = readlane(bampo, 3 * b + 2), amp_n = readlane(bampn, 3 * b + 2);
 
     // ---- likelihood difference -----------------------------------------------
     float dll;
@@ -418,8 +433,9 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
       }
       dll = (float)(new_ll - cur_ll);
     } else {
-      const int fh0 = ifloor_clamped(P.h), fw0 = ifloor_clamped(P.w);
-      const int fh1 = ifloor_clamped(P.hn), fw1 = ifloor_clamped(P.wn);
+      const int flh = readlane(bfl, 3 * b), flw = readlane(bfl, 3 * b + 1);
+      const int fh0 = (int)(int16_t)(flh & 0xffff), fh1 = flh >> 16;
+      const int fw0 = (int)(int16_t)(flw & 0xffff), fw1 = flw >> 16;
       r0 = max(min(fh0, fh1) - m.R, 0);
       const int r1 = min(max(fh0, fh1) + m.R, m.H - 1);
       c0 = max(min(fw0, fw1) - m.R, 0);
@@ -572,8 +588,9 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
         for (int i = 0; i < kSlots; ++i)
           if (i < nslots) lam[s_pix[i]] = s_lam[i];
         if (npos > kSlots * kWave) {
-          const int fh0 = ifloor_clamped(P.h), fw0 = ifloor_clamped(P.w);
-          const int fh1 = ifloor_clamped(P.hn), fw1 = ifloor_clamped(P.wn);
+          const int flh = readlane(bfl, 3 * b), flw = readlane(bfl, 3 * b + 1);
+          const int fh0 = (int)(int16_t)(flh & 0xffff), fh1 = flh >> 16;
+          const int fw0 = (int)(int16_t)(flw & 0xffff), fw1 = flw >> 16;
           const int ao_h = fh0 - m.R - r0, ao_w = fw0 - m.R - c0;
           const int an_h = fh1 - m.R - r0, an_w = fw1 - m.R - c0;
           const float inv_bw = 1.0f / (float)bw;
@@ -590,20 +607,17 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
         cur_ll += (double)dll;
         wave_sync();
       }
-      const bool me = lane == P.j;
-      sh = me ? P.hn : sh;
-      sw = me ? P.wn : sw;
-      sfx = me ? P.fn : sfx;
-      lfx = me ? P.lfn : lfx;
-      const float nph_h = readlane(bph, 3 * b), nlZ_h = readlane(blZ, 3 * b);
-      const float nph_w = readlane(bph, 3 * b + 1), nlZ_w = readlane(blZ, 3 * b + 1);
-      const float nph_f = readlane(bph, 3 * b + 2), nlZ_f = readlane(blZ, 3 * b + 2);
-      ph_h = me ? nph_h : ph_h;
-      lZ_h = me ? nlZ_h : lZ_h;
-      ph_w = me ? nph_w : ph_w;
-      lZ_w = me ? nlZ_w : lZ_w;
-      ph_f = me ? nph_f : ph_f;
-      lZ_f = me ? nlZ_f : lZ_f;
+      // source j takes the proposal and its proposal caches (v_writelane)
+      sh = writelane(P.hn, P.j, sh);
+      sw = writelane(P.wn, P.j, sw);
+      sfx = writelane(P.fn, P.j, sfx);
+      lfx = writelane(readlane(blf, 3 * b + 2), P.j, lfx);
+      ph_h = writelane(readlane(bph, 3 * b), P.j, ph_h);
+      lZ_h = writelane(readlane(blZ, 3 * b), P.j, lZ_h);
+      ph_w = writelane(readlane(bph, 3 * b + 1), P.j, ph_w);
+      lZ_w = writelane(readlane(blZ, 3 * b + 1), P.j, lZ_w);
+      ph_f = writelane(readlane(bph, 3 * b + 2), P.j, ph_f);
+      lZ_f = writelane(readlane(blZ, 3 * b + 2), P.j, lZ_f);
       dirty |= 1ull << P.j;
     }
   }

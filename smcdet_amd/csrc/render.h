@@ -15,6 +15,11 @@ namespace smcdet {
 __device__ __forceinline__ int ifloor_clamped(float v) {
   return (int)fmaxf(fminf(floorf(v), 1.0e6f), -1.0e6f);
 }
+// floor clamped to 16 bits (two anchors packed per int; locations lie within
+// a few pixels of the tile, and anchors this far out give empty windows either way)
+__device__ __forceinline__ int ifloor16(float v) {
+  return (int)fmaxf(fminf(floorf(v), 16383.0f), -16384.0f);
+}
 
 // lam[p] += amp * psf(|p + 0.5 - (h, w)|) over the source's clipped window
 // (LDS read-modify-write; used for tiles above 1024 pixels or S > 64).
