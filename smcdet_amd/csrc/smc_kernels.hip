@@ -318,8 +318,22 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
     // (what torch's CPU cumsum does), contiguous chunk per thread, in place
     const int chunk = (N + kTB - 1) / kTB;
     const int b0 = min((int)threadIdx.x * chunk, N), b1 = min(b0 + chunk, N);
+    // chunks of 8 (N = 4096) move as two 16-byte LDS accesses per thread
+    const bool vec8 = chunk == 8 && (N & 7) == 0;
+    float cv[8];
     double part = 0.0;
-    for (int i = b0; i < b1; ++i) part += (double)buf[i];
+    if (vec8) {
+      if (b0 < b1) {
+        const float4 v0 = *reinterpret_cast<const float4*>(buf + b0);
+        const float4 v1 = *reinterpret_cast<const float4*>(buf + b0 + 4);
+        cv[0] = v0.x; cv[1] = v0.y; cv[2] = v0.z; cv[3] = v0.w;
+        cv[4] = v1.x; cv[5] = v1.y; cv[6] = v1.z; cv[7] = v1.w;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) part += (double)cv[i];
+      }
+    } else {
+      for (int i = b0; i < b1; ++i) part += (double)buf[i];
+    }
     double incl = part;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -334,9 +348,21 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
     double base = 0.0;
     for (int i = 0; i < wave; ++i) base += red.d[k][i][0];
     double run = base + incl - part;
-    for (int i = b0; i < b1; ++i) {
-      run += (double)buf[i];
-      buf[i] = (float)run;
+    if (vec8) {
+      if (b0 < b1) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          run += (double)cv[i];
+          cv[i] = (float)run;
+        }
+        *reinterpret_cast<float4*>(buf + b0) = make_float4(cv[0], cv[1], cv[2], cv[3]);
+        *reinterpret_cast<float4*>(buf + b0 + 4) = make_float4(cv[4], cv[5], cv[6], cv[7]);
+      }
+    } else {
+      for (int i = b0; i < b1; ++i) {
+        run += (double)buf[i];
+        buf[i] = (float)run;
+      }
     }
     __syncthreads();
     float U = 0.f;
@@ -361,7 +387,17 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
       int* slot = reinterpret_cast<int*>(buf + N);  // N+1 ints
       const float Nf = (float)N;
       auto un = [&](int n) { return ((float)n + U) / Nf; };
+      // For N a power of two the division is an exact scaling:
+      // u_n <= b  <=>  fl(n + U) <= b*N (exact), and n <= fl(n + U) <= n + 1,
+      // so every n < floor(b*N) counts and only n = floor(b*N) needs a test.
+      const bool pow2 = (N & (N - 1)) == 0;
       auto cnt = [&](float b) {
+        if (pow2) {
+          const float B = b * Nf;
+          int c = (int)fminf(fmaxf(floorf(B), 0.f), Nf);
+          c += (c < N && (float)c + U <= B) ? 1 : 0;
+          return c;
+        }
         int c = (int)fminf(fmaxf(floorf(b * Nf - U), 0.f), Nf);
         while (c > 0 && un(c - 1) > b) --c;
         while (c < N && un(c) <= b) ++c;
@@ -370,19 +406,28 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
       for (int i = threadIdx.x; i <= N; i += kTB) slot[i] = 0;
       __syncthreads();
       SMC_TRACE(trow, 6);
-      if (b0 < b1) {
-        int cprev = cnt(buf[b0]);
-        for (int i = b0; i < b1; ++i) {
-          const int cnext = (i + 1 < N) ? cnt(buf[i + 1]) : -1;
-          if (cnext != cprev) slot[cprev] = i + 1;
-          cprev = cnext;
-        }
+      for (int i = threadIdx.x; i < N; i += kTB) {
+        const int ci = cnt(buf[i]);
+        const int cnext = (i + 1 < N) ? cnt(buf[i + 1]) : -1;
+        if (cnext != ci) slot[ci] = i + 1;
       }
       __syncthreads();
       SMC_TRACE(trow, 7);
       // prefix max over slot[0..N-1], contiguous chunk per thread
       int pm = 0;
-      for (int i = b0; i < b1; ++i) pm = max(pm, slot[i]);
+      int sv[8];
+      if (vec8) {
+        if (b0 < b1) {
+          const int4 v0 = *reinterpret_cast<const int4*>(slot + b0);
+          const int4 v1 = *reinterpret_cast<const int4*>(slot + b0 + 4);
+          sv[0] = v0.x; sv[1] = v0.y; sv[2] = v0.z; sv[3] = v0.w;
+          sv[4] = v1.x; sv[5] = v1.y; sv[6] = v1.z; sv[7] = v1.w;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) pm = max(pm, sv[i]);
+        }
+      } else {
+        for (int i = b0; i < b1; ++i) pm = max(pm, slot[i]);
+      }
       int incl_m = pm;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
@@ -397,9 +442,21 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
       if (lane == 0) run_m = 0;
       for (int i = 0; i < wave; ++i) run_m = max(run_m, red.i[k2][i]);
       // in place: slot[i] becomes idx[i] (each thread owns its chunk)
-      for (int i = b0; i < b1; ++i) {
-        run_m = max(run_m, slot[i]);
-        slot[i] = min(run_m, N - 1);
+      if (vec8) {
+        if (b0 < b1) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            run_m = max(run_m, sv[i]);
+            sv[i] = min(run_m, N - 1);
+          }
+          *reinterpret_cast<int4*>(slot + b0) = make_int4(sv[0], sv[1], sv[2], sv[3]);
+          *reinterpret_cast<int4*>(slot + b0 + 4) = make_int4(sv[4], sv[5], sv[6], sv[7]);
+        }
+      } else {
+        for (int i = b0; i < b1; ++i) {
+          run_m = max(run_m, slot[i]);
+          slot[i] = min(run_m, N - 1);
+        }
       }
       __syncthreads();
       SMC_TRACE(trow, 8);
