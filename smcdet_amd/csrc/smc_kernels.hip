@@ -129,6 +129,18 @@ __device__ __forceinline__ V tree_sum(V (&x)[PER]) {
   return x[0];
 }
 
+// a / b by v_rcp_f64 + two Newton steps + one residual correction: the
+// quotient to the last bit or so, without the IEEE division sequence's scale /
+// fixup steps on the latency-bound Brent path (b = 0 or inf gives a NaN/inf
+// step, which the Brent tests reject exactly as they reject scipy's)
+__device__ __forceinline__ double ddiv(double a, double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  r = fma(fma(-b, r, 1.0), r, r);
+  r = fma(fma(-b, r, 1.0), r, r);
+  const double q = a * r;
+  return fma(fma(-b, q, a), r, q);
+}
+
 // Each thread's log-likelihoods (i = threadIdx.x + j*kTB) live in registers
 // for the whole tempering search.
 template <int PER>
@@ -162,7 +174,7 @@ __device__ __forceinline__ double block_ess_objective(const TileLL<PER>& ll, int
   float s1 = tree_sum(e1), s2 = tree_sum(e2);
   block_sum2f(s1, s2, red, parity);
   const double d1 = (double)s1;
-  return d1 * d1 / (double)s2 - thr;
+  return ddiv(d1 * d1, (double)s2) - thr;
 }
 
 // scipy.optimize.brentq (scipy/optimize/Zeros/brentq.c, the algorithm the
@@ -191,11 +203,11 @@ __device__ double block_brentq(F&& f, double xa, double xb, double fa, double fb
     if (fabs(spre) > delta && fabs(fcur) < fabs(fpre)) {
       double stry;
       if (xpre == xblk) {
-        stry = -fcur * (xcur - xpre) / (fcur - fpre);  // interpolate
+        stry = ddiv(-fcur * (xcur - xpre), fcur - fpre);  // interpolate
       } else {                                         // extrapolate
-        const double dpre = (fpre - fcur) / (xpre - xcur);
-        const double dblk = (fblk - fcur) / (xblk - xcur);
-        stry = -fcur * (fblk * dblk - fpre * dpre) / (dblk * dpre * (fblk - fpre));
+        const double dpre = ddiv(fpre - fcur, xpre - xcur);
+        const double dblk = ddiv(fblk - fcur, xblk - xcur);
+        stry = ddiv(-fcur * (fblk * dblk - fpre * dpre), dblk * dpre * (fblk - fpre));
       }
       if (2 * fabs(stry) < fmin(fabs(spre), 3 * fabs(sbis) - delta)) {
         spre = scur;
