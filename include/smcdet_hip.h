@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 4
+#define SMCDET_ABI_VERSION 5
 
 /* status codes */
 #define SMCDET_OK 0
@@ -54,6 +54,17 @@ extern "C" {
  * fixed-count kernel with S = s (kernel.py:35-37); count 0 never moves.
  * Used by the count-stratified sampler (CS-SMC). */
 #define SMCDET_MH_COMPONENT_BY_COUNT 2u
+/* independent stopping: tiles whose temperature is already 1 are not mutated
+ * (their particles are only gathered through `ancestors`) */
+#define SMCDET_MH_SKIP_DONE 4u
+
+/* temper_reweight flags */
+/* independent stopping: a tile that entered at temperature 1 keeps it (delta
+ * 0), gets uniform weights, an unchanged log Z and identity resampling
+ * indices, so its final particles stay put while the other tiles run on.
+ * Without it (the reference, sampler.py:230) such tiles are resampled and
+ * mutated at temperature 1 until every tile has finished. */
+#define SMCDET_SMC_FREEZE_DONE 1u
 /* diagnostic ablations (timing only; results are NOT valid samples) */
 #define SMCDET_MH_ABLATE_LIKELIHOOD 256u /* skip the delta-likelihood passes */
 #define SMCDET_MH_ABLATE_PROPOSAL 512u   /* skip the truncated-normal proposal math */
@@ -200,13 +211,14 @@ int smcdet_resample_index(const float* weights, int32_t T, int32_t N,
                           const float* u, int64_t* idx, void* stream);
 
 /* temper + update_weights (+ resample index when idx != null) fused: one
- * launch per SMC iteration instead of three. */
+ * launch per SMC iteration instead of three.  flags: SMCDET_SMC_*. */
 int smcdet_temper_reweight(const float* loglik, float* temperature,
                            float* temperature_prev, float* log_weights_unnorm,
                            float* weights, float* ess, float* log_norm_const,
                            int32_t T, int32_t N, double ess_threshold,
                            int32_t resample_method, uint64_t seed,
-                           uint64_t offset, int64_t* idx, void* stream);
+                           uint64_t offset, int64_t* idx, uint32_t flags,
+                           void* stream);
 
 /* Gather of the resampled state (smcdet/sampler.py:150-169). */
 int smcdet_gather(const int64_t* idx, int32_t T, int32_t N, int32_t S,

@@ -100,6 +100,18 @@ def main():
         m = sid == v
         simd_stats.append((m.sum(), end[m].min(), end[m].max(), npos[m].sum()))
     st = np.array(simd_stats, dtype=np.float64)
+    # placement hypothesis: workgroup b (4 waves) lands on CU slot b % 256 and
+    # wave w of it on SIMD w, so SIMD-mates are waves (b + 256 k, w)
+    wave_idx = np.arange(len(sid))
+    b_of, w_of = wave_idx // 4, wave_idx % 4
+    hyp = (b_of % 256) * 4 + w_of
+    ok = 0
+    for v in np.unique(sid):
+        m = np.nonzero(sid == v)[0]
+        ok += int(len(np.unique(hyp[m])) == 1)
+    out["placement_hypothesis_simds_matching"] = f"{ok}/{len(np.unique(sid))}"
+    out["placement_sample"] = [[int(i), int(xid[i]), int(se[i]), int(sh[i]), int(cu[i]),
+                                int(simd[i])] for i in list(range(0, 16)) + [1024, 1025, 2048]]
     out["per_simd"] = {
         "n_simds": int(len(st)), "waves_per_simd_pctl": np.percentile(st[:, 0], [0, 50, 100]).tolist(),
         "first_end_us_pctl": np.percentile(st[:, 1], [0, 10, 50, 90, 100]).round(1).tolist(),

@@ -22,6 +22,8 @@ SMCDET_RESAMPLE_MULTINOMIAL = 0
 SMCDET_RESAMPLE_SYSTEMATIC = 1
 SMCDET_MH_FULL_RECOMPUTE = 1
 SMCDET_MH_COMPONENT_BY_COUNT = 2
+SMCDET_MH_SKIP_DONE = 4
+SMCDET_SMC_FREEZE_DONE = 1
 
 c_f = ctypes.c_float
 c_i = ctypes.c_int32
@@ -70,7 +72,7 @@ _SIGS = {
     "smcdet_update_weights": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p], c_i),
     "smcdet_resample_index": ([c_p, c_i, c_i, c_i, c_u64, c_u64, c_p, c_p, c_p], c_i),
     "smcdet_temper_reweight": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_d, c_i, c_u64,
-                                c_u64, c_p, c_p], c_i),
+                                c_u64, c_p, c_u32, c_p], c_i),
     "smcdet_gather": ([c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
     "smcdet_count_posterior": ([c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_u64, c_u64, c_p, c_p,
                                 c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),

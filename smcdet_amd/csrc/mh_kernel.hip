@@ -56,6 +56,7 @@ struct MhArgs {
   uint32_t ablate;                   // SMCDET_MH_ABLATE_* (diagnostics)
   int by_count;                      // SMCDET_MH_COMPONENT_BY_COUNT
   int scalar_slots;                  // SMCDET_MH_SCALAR_SLOTS (diagnostic)
+  int skip_done;                     // SMCDET_MH_SKIP_DONE
   const float* img;                  // [T,H,W]
   const float* temperature;          // [T]
   const int64_t* ancestors;          // [T,N] or null
@@ -227,7 +228,10 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   // range of the moved component: 0..S-1 (kernel.py:35-37), or 0..count-1
   // for count-stratified populations padded to S sources (count 0: no moves)
   const int Sj = a.by_count ? min(max((int)count, 0), S) : S;
-  const int K = Sj > 0 ? a.K : 0;
+  const float tau = a.temperature[t];
+  // independent stopping: a tile already at temperature 1 keeps its
+  // (resampled) particles unchanged (SMCDET_MH_SKIP_DONE)
+  const int K = (Sj > 0 && !(a.skip_done && tau >= 1.0f)) ? a.K : 0;
 
   // ---- particle state: lane s holds source s --------------------------------
   float sh = 0.f, sw = 0.f, sfx = 0.f;
@@ -244,7 +248,6 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   float lfx = fast_log(sfx);
   SMC_TRACE(trow, 2);
 
-  const float tau = a.temperature[t];
   double cur_ll = 0.0;  // tracked only in FULL mode (incremental mode works on deltas)
   if constexpr (!FULL) {
     if (a.rate_in) {
@@ -813,6 +816,7 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
   a.ablate = flags & (SMCDET_MH_ABLATE_LIKELIHOOD | SMCDET_MH_ABLATE_PROPOSAL);
   a.by_count = (flags & SMCDET_MH_COMPONENT_BY_COUNT) != 0;
   a.scalar_slots = (flags & SMCDET_MH_SCALAR_SLOTS) != 0;
+  a.skip_done = (flags & SMCDET_MH_SKIP_DONE) != 0;
   rc = a.m.model == SMCDET_MODEL_M71
            ? launch_mh<SMCDET_MODEL_M71>(a, replay != nullptr, full, grid, lds, st)
            : launch_mh<SMCDET_MODEL_POISSON>(a, replay != nullptr, full, grid, lds, st);

@@ -42,6 +42,7 @@ struct TileArgs {
   uint64_t offset;
   const float* u;            // replay uniforms or null
   int64_t* idx;              // [T,N]
+  uint32_t smc_flags;        // SMCDET_SMC_*
 };
 
 // Workgroup reductions with ONE barrier each: wave DPP reductions -> per-wave
@@ -240,6 +241,21 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
 
   [[maybe_unused]] const int trow = threadIdx.x < kWave ? t : -1;
   SMC_TRACE(trow, 0);
+  // independent stopping: a finished tile stays as it is (uniform weights of
+  // its final resampled population, identity ancestors, log Z unchanged)
+  if ((a.smc_flags & SMCDET_SMC_FREEZE_DONE) && a.temperature[t] >= 1.0f) {
+    if ((a.flags & kDoTemper) && threadIdx.x == 0) a.temperature_prev[t] = a.temperature[t];
+    if (a.flags & kDoWeights) {
+      for (int i = threadIdx.x; i < N; i += kTB) {
+        a.log_w[(size_t)t * N + i] = 0.0f;
+        a.weights[(size_t)t * N + i] = 1.0f / (float)N;
+      }
+      if (threadIdx.x == 0) a.ess[t] = (float)N;
+    }
+    if (a.flags & kDoResample)
+      for (int i = threadIdx.x; i < N; i += kTB) a.idx[(size_t)t * N + i] = i;
+    return;
+  }
   TileLL<PER> ll;
   if (a.flags & (kDoTemper | kDoWeights)) {
     const float* llg = a.loglik + (size_t)t * N;
@@ -716,7 +732,7 @@ int smcdet_temper_reweight(const float* loglik, float* temperature, float* tempe
                            float* log_weights_unnorm, float* weights, float* ess,
                            float* log_norm_const, int32_t T, int32_t N, double ess_threshold,
                            int32_t resample_method, uint64_t seed, uint64_t offset, int64_t* idx,
-                           void* stream) {
+                           uint32_t flags, void* stream) {
   if (!loglik || !temperature || !temperature_prev || !log_weights_unnorm || !weights || !ess ||
       !log_norm_const)
     return set_error(SMCDET_EINVAL, "null buffer");
@@ -741,6 +757,7 @@ int smcdet_temper_reweight(const float* loglik, float* temperature, float* tempe
   a.k1 = (uint32_t)(seed >> 32);
   a.offset = offset;
   a.idx = idx;
+  a.smc_flags = flags;
   return launch_tile(a, (hipStream_t)stream);
 }
 

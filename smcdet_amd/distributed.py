@@ -52,7 +52,8 @@ class TileShardedSMC:
 
     def __init__(self, image, tile_dim, Prior, ImageModel, MutationKernel, num_catalogs,
                  ess_threshold_prop, resample_method, flux_detection_threshold, max_smc_iters,
-                 print_every=10 ** 9, *, lockstep=False, seed=None, device=None, group=None):
+                 print_every=10 ** 9, *, lockstep=False, seed=None, device=None, group=None,
+                 **sampler_kwargs):
         self.rank, self.world_size = world()
         self.group = group
         self.lockstep = lockstep
@@ -68,7 +69,7 @@ class TileShardedSMC:
         self.sampler = SMCsampler.from_tiles(
             local.reshape(1, -1, tile_dim, tile_dim), Prior, ImageModel, MutationKernel,
             num_catalogs, ess_threshold_prop, resample_method, flux_detection_threshold,
-            max_smc_iters, print_every, seed=seed, device=device)
+            max_smc_iters, print_every, seed=seed, device=device, **sampler_kwargs)
         if lockstep and self.world_size > 1:
             self.sampler._keep_going = self._keep_going_global
 

@@ -93,7 +93,7 @@ class SingleComponentMH(object):
 
     def run(self, data, counts, locs, fluxes, temperature, log_target=None, *, prior=None,
             image_model=None, ancestors=None, replay=None, want_loglik=True, rate_in=None,
-            rate_out=None):
+            rate_out=None, flags=0):
         """kernel.py:26-130.  ancestors [numH,numW,N] (int64, optional) gathers
         the starting state (a fused resample); replay = dict(comp, uloc, uflux,
         uacc) replays recorded draws; rate_in / rate_out [numH,numW,N,H*W]
@@ -135,9 +135,11 @@ class SingleComponentMH(object):
                               _hip.ptr(ru[2]).value)
         off = self.rng.take(self.num_iters)
         cm, cp, ch = image_model._cmodel(), prior._cprior(), self._cmh(prior)
+        extra_flags = flags
         flags = (_hip.SMCDET_MH_FULL_RECOMPUTE if self.full_recompute else 0) | self.debug_flags
         if self.component_by_count:
             flags |= _hip.SMCDET_MH_COMPONENT_BY_COUNT
+        flags |= int(extra_flags)
         ev = self.launch_events
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -33,7 +33,7 @@ class SMCsampler(object):
     def __init__(self, image, tile_dim, Prior, ImageModel, MutationKernel, num_catalogs,
                  ess_threshold_prop, resample_method, flux_detection_threshold, max_smc_iters,
                  print_every=5, *, seed=None, device=None, fused=True, persist_rate_images=True,
-                 rate_refresh_every=8):
+                 rate_refresh_every=8, stopping="lockstep"):
         if device is None:
             device = image.device if image.is_cuda else torch.device(
                 "cuda", torch.cuda.current_device())
@@ -67,6 +67,13 @@ class SMCsampler(object):
         self.print_every = print_every
         self.has_run = False
 
+        # "lockstep": the reference's rule (sampler.py:230) -- every tile is
+        # resampled and mutated until all tiles reach temperature 1;
+        # "independent": a tile stops (its final resampled particles stay put)
+        # as soon as it reaches temperature 1 -- less work, same per-tile target
+        if stopping not in {"lockstep", "independent"}:
+            raise ValueError("stopping must be either lockstep or independent.")
+        self.stopping = stopping
         self.rng = PhiloxStream(seed)
         self.MutationKernel.rng = self.rng
         self.fused = fused
@@ -131,6 +138,8 @@ class SMCsampler(object):
         self.log_normalizing_constant = self._zeros_tiles()
         self.ess = torch.full((nH, nW), float(N), device=self.device)
         self._pending_idx = None
+        # SMC iteration at which each tile reached temperature 1 (-1: not yet)
+        self.iters_per_tile = torch.full((nH, nW), -1, device=self.device, dtype=torch.int32)
 
     def log_target(self, data, counts, locs, fluxes, temperature):
         """sampler.py:87-91."""
@@ -165,6 +174,7 @@ class SMCsampler(object):
             "smcdet_temper")
         self.temperature_prev = prev_t
         self.temperature = new_t
+        self._mark_finished()
 
     def update_weights(self):
         """sampler.py:181-196."""
@@ -229,6 +239,8 @@ class SMCsampler(object):
         """sampler.py:171-179."""
         rin, rout = self._rate_buffers()
         kw = {} if rout is None else {"rate_in": rin, "rate_out": rout}
+        if self.stopping == "independent":
+            kw["flags"] = _hip.SMCDET_MH_SKIP_DONE
         self.locs, self.fluxes, self.mutation_acc_rates = self.MutationKernel.run(
             self.tiled_image, self.counts, self.locs, self.fluxes, self.temperature,
             self.log_target, ancestors=ancestors, **kw)
@@ -265,11 +277,19 @@ class SMCsampler(object):
             _hip.ptr(self.loglik), _hip.ptr(new_t), _hip.ptr(prev_t),
             _hip.ptr(self.weights_log_unnorm), _hip.ptr(self.weights), _hip.ptr(self.ess),
             _hip.ptr(self.log_normalizing_constant), self._T, N, float(self.ess_threshold),
-            self._method_code(), self.rng.seed, off, _hip.ptr(idx), _hip.stream_of(new_t)),
-            "smcdet_temper_reweight")
+            self._method_code(), self.rng.seed, off, _hip.ptr(idx),
+            _hip.SMCDET_SMC_FREEZE_DONE if self.stopping == "independent" else 0,
+            _hip.stream_of(new_t)), "smcdet_temper_reweight")
         self.temperature_prev = prev_t
         self.temperature = new_t
         self._pending_idx = idx
+        self._mark_finished()
+
+    def _mark_finished(self):
+        it = getattr(self, "iters_per_tile", None)
+        if it is not None:
+            done = (self.temperature >= 1) & (it < 0)
+            it.masked_fill_(done, int(getattr(self, "iter", 0)))
 
     def prune(self, locs, fluxes):
         """sampler.py:198-219: detectable (flux > threshold) sources strictly
@@ -315,6 +335,8 @@ class SMCsampler(object):
                 self.mutate(ancestors=idx)
                 self._temper_reweight(with_resample=True)
         else:
+            if self.stopping != "lockstep":
+                raise NotImplementedError("independent stopping runs on the fused schedule")
             self.temper()
             self.update_weights()
             while self._keep_going() and self.iter <= self.max_smc_iters:

@@ -531,12 +531,14 @@ def gen_stats(which, seeds):
         pr = basic_prior(16, 3, 3)
         mk = lambda: SingleComponentMH(100, 0.1, 100, pr.flux_scale, 1e6)  # noqa: E731
         model, tile, N, method = basic_model(16), 16, 256, "systematic"
-    elif which == "m71":
+    elif which in ("m71", "m71_multinomial"):
         res = m71_truth_image(8, 0)
         img = res[-1][0]
         pr = m71_prior(8, 10, 10)
         mk = lambda: SingleComponentMH(100, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])  # noqa
-        model, tile, N, method = m71_model(8), 8, 1000, "systematic"
+        model, tile, N = m71_model(8), 8, 1000
+        # notebooks/smc.ipynb cell 7 resamples multinomially
+        method = "systematic" if which == "m71" else "multinomial"
     else:
         raise ValueError(which)
     rows = []

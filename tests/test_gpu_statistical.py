@@ -4,6 +4,7 @@ tests/golden/stats_{basic,m71}.json hold 20 seeded runs of the REFERENCE
 SMCsampler.run() (CPU, float32) on a fixed image (make_golden.py stats):
   basic: 16x16 Poisson ImageModel + ParetoStarPrior(3,3), N=256, K=100, systematic
   m71:   8x8 M71ImageModel + M71Prior(10,10), N=1000, K=100, systematic
+  m71_multinomial: the same with multinomial resampling (notebooks/smc.ipynb cell 7)
 (make_golden.py passes the M71 flux_detection_threshold to both samplers.)
 Random streams cannot match torch's, so parity is distributional: mean log Z
 within 1% and within 3 pooled standard errors; non-final ESS = rho*N; final
@@ -60,8 +61,10 @@ def _se(a, b):
     return np.sqrt(np.var(a, ddof=1) / len(a) + np.var(b, ddof=1) / len(b))
 
 
-@pytest.mark.parametrize("which", ["basic", "m71"])
+@pytest.mark.parametrize("which", ["basic", "m71", "m71_multinomial"])
 def test_statistical_parity_vs_reference(which):
+    if not os.path.exists(os.path.join(GOLDEN, f"stats_{which}.json")):
+        pytest.skip(f"stats_{which}.json not generated")
     ref = _load(which)
     cfg = ref["config"]
     image = torch.tensor(ref["image"], dtype=torch.float32, device="cuda")
