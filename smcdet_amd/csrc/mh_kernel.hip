@@ -25,9 +25,12 @@
 //     whose error scales with the change, not with the absolute terms.  (Mode SMCDET_MH_FULL_RECOMPUTE instead
 //     re-renders every source each step, as the reference does.)
 //   * accept iff U <= min(1, exp(log alpha)) (kernel.py:114-116).
-// The rate image is rebuilt from scratch at the start of each sweep; the
-// returned loglik_out is summed over the final rate image (fresh full render
-// in FULL_RECOMPUTE mode).
+// The rate image comes from the ancestor's persisted image (rate_in) or a
+// fresh render; the returned loglik_out is summed over the final rate image
+// (fresh full render in FULL_RECOMPUTE mode).  The union-window positions run
+// two per lane in packed f32 arithmetic (position_delta2), and everything
+// wave-uniform about an iteration (anchors, amplitudes, prior and Hastings
+// terms) is computed once per proposal batch in the batch's lanes.
 #include <math.h>
 
 #include <type_traits>

@@ -3,7 +3,7 @@
 // systematic and multinomial resampling (sampler.py:127-169) and pruning
 // (sampler.py:198-219).
 //
-// One 256-thread workgroup per tile does temper -> reweight -> resample
+// One 512-thread workgroup per tile does temper -> reweight -> resample
 // indices in one launch, so an SMC iteration needs no host round trip (the
 // reference copies the log-likelihoods to the host and runs scipy brentq per
 // tile).  ESS(delta) is monotone, but brentq stops within xtol = 1e-6 of the
