@@ -42,16 +42,22 @@ M71 = dict(flux_alpha=0.21411753249015655, flux_lower=0.06291294097900389,
            psf_radius=8, noise_additive=1.0000007072408224e-10,
            noise_multiplicative=1.936462640762329)
 COUNTS_RATE_C2 = 5.0 / (40 * 40)
+M71_COUNTS_RATE = 0.030264640226960182  # notebooks/smc.ipynb cell 2
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md (spec)
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md (vector FP32, spec)
 B_ALG_PER_STEP = 248        # SURVEY §8d, S=10
 F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
-PMC_FILE = "pmc_mh_r01.json"  # rocprofv3 FETCH_SIZE+WRITE_SIZE per MH launch (scripts/profile.sh)
+PMC_FILE = "pmc_mh_r01_s2.json"  # rocprofv3 FETCH_SIZE+WRITE_SIZE per MH launch (scripts/profile.sh)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    # c2 (default, the headline): one 32x32 tile per GPU.  c4 / c5 are the
+    # BASELINE.json configs[3] / [4] run as extra lines: batches of 8x8 M71
+    # tiles (N=4096, S=10) and count-stratified SMC over 8x8 tiles (counts
+    # 0..6, 8192 particles per count), per GPU.
+    ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--particles", type=int, default=4096)
@@ -141,6 +147,69 @@ def cpu_baseline(args, image_tile, seconds):
                       f"iterations, {H}x{H} tile, S={S}, tau=0.3 ({dt:.1f} s)"}
 
 
+def build_sampler(args, dev, rank):
+    """(sampler, particle-steps per SMC step, workload description)."""
+    from smcdet_amd.sampler import SMCsampler
+    p = M71
+    if args.workload == "c2":
+        H, S, Np, K = args.tile, args.sources, args.particles, args.mh_iters
+        tps = int(round(args.tiles_per_gpu ** 0.5))
+        model, prior, truth, MH = make_models(H, S)
+        image = synthetic_image(model, truth, H, tps, 1000 + rank, dev, max_sources=S)
+        mh = MH(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"], full_recompute=args.full_recompute)
+        s = SMCsampler(image, H, prior, model, mh, Np, 0.5, "systematic",
+                       p["flux_detection_threshold"], 10 ** 9, print_every=10 ** 9,
+                       seed=12345 + rank, device=dev)
+        T = tps * tps
+        return s, mh, T * Np * K, image[:H, :H], dict(
+            workload=f"C2: {T} x {H}x{H} tile(s)/GPU, S={S}, N={Np}, {K} MH iters per SMC step, "
+                     "systematic, rho=0.5", tiles_per_gpu=T, particles=Np, tile=H, sources=S,
+            mh_iters=K)
+    # 8x8 M71 tiles at the real M71 source density (experiments/m71synthetic/
+    # generate_images.py:27-67: truth from M71Prior(0, 100))
+    from smcdet_amd.images import M71ImageModel
+    from smcdet_amd.kernel import SingleComponentMH
+    from smcdet_amd.prior import M71Prior
+    H, K, B = 8, args.mh_iters, max(1, args.tiles_per_gpu)
+    model = M71ImageModel(image_height=H, image_width=H, background=p["background"],
+                          psf_radius=p["psf_radius"], adu_per_nmgy=p["adu_per_nmgy"],
+                          psf_params=p["psf_params"], noise_additive=p["noise_additive"],
+                          noise_multiplicative=p["noise_multiplicative"])
+    truth = M71Prior(min_objects=0, max_objects=100, counts_rate=M71_COUNTS_RATE, image_height=H,
+                     image_width=H, flux_alpha=p["flux_alpha"],
+                     flux_lower=p["flux_detection_threshold"], flux_upper=p["flux_upper"], pad=4)
+    torch.manual_seed(2000 + rank)
+    c, l, f = truth.sample(num_catalogs=B, device=dev)
+    images = model.sample(l, f)[0, 0].permute(2, 0, 1).contiguous()       # [B, 8, 8]
+    mh = SingleComponentMH(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"])
+    if args.workload == "c4":
+        S, Np = 10, 4096
+        prior = M71Prior(min_objects=S, max_objects=S, counts_rate=M71_COUNTS_RATE,
+                         image_height=H, image_width=H, flux_alpha=p["flux_alpha"],
+                         flux_lower=p["flux_lower"], flux_upper=p["flux_upper"], pad=4)
+        s = SMCsampler.from_tiles(images.reshape(1, B, H, H), prior, model, mh, Np, 0.5,
+                                  "systematic", p["flux_detection_threshold"], 10 ** 9,
+                                  10 ** 9, seed=12345 + rank, device=dev)
+        return s, mh, B * Np * K, images[0], dict(
+            workload=f"C4: {B} x 8x8 M71 tiles/GPU (batched), S={S}, N={Np}, {K} MH iters per "
+                     "SMC step, systematic, rho=0.5", tiles_per_gpu=B, particles=Np, tile=H,
+            sources=S, mh_iters=K)
+    from smcdet_amd.cssmc import CountStratifiedSMC
+    smax, Np = 6, 8192
+    prior = M71Prior(min_objects=0, max_objects=smax, counts_rate=M71_COUNTS_RATE,
+                     image_height=H, image_width=H, flux_alpha=p["flux_alpha"],
+                     flux_lower=p["flux_lower"], flux_upper=p["flux_upper"], pad=4)
+    cs = CountStratifiedSMC(images.reshape(1, B, H, H), H, prior, model, mh, Np, 0.5,
+                            "systematic", p["flux_detection_threshold"], 10 ** 9, 10 ** 9,
+                            seed=12345 + rank, device=dev)
+    NS = smax + 1
+    return cs.sampler, cs.MutationKernel, B * NS * Np * K, images[0], dict(
+        workload=f"C5: CS-SMC over {B} x 8x8 M71 tiles/GPU, counts 0..{smax} "
+                 f"({NS} strata as tiles, S={smax}), N={Np} per count, {K} MH iters per SMC step, "
+                 "systematic, rho=0.5", tiles_per_gpu=B, particles=Np * NS, tile=H, sources=smax,
+        mh_iters=K)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -154,16 +223,9 @@ def main():
     dev = torch.device("cuda", local if dist else 0)
     torch.cuda.set_device(dev)
 
-    from smcdet_amd.sampler import SMCsampler
-    H, S, Np, K = args.tile, args.sources, args.particles, args.mh_iters
-    tps = int(round(args.tiles_per_gpu ** 0.5))
-    model, prior, truth, MH = make_models(H, S)
-    image = synthetic_image(model, truth, H, tps, 1000 + rank, dev, max_sources=S)
-    mh = MH(K, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"],
-            full_recompute=args.full_recompute)
-    s = SMCsampler(image, H, prior, model, mh, Np, 0.5, "systematic",
-                   M71["flux_detection_threshold"], 10 ** 9, print_every=10 ** 9,
-                   seed=12345 + rank, device=dev)
+    if args.workload != "c2" and args.tiles_per_gpu == 1:
+        args.tiles_per_gpu = 42  # 332 M71 cutouts over 8 GPUs (manuscript.tex:562)
+    s, mh, steps_per_step, cpu_tile, cfg = build_sampler(args, dev, rank)
     s.initialize()
     s._temper_reweight(with_resample=True)
 
@@ -197,21 +259,24 @@ def main():
         elapsed = float(t)
     mh_ms = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
 
-    T = tps * tps
-    steps_per_step = T * Np * K
     value = world * steps_per_step * args.steps / elapsed
     launch_steps = steps_per_step  # particle-steps per MH launch
-    achieved_gbs = B_ALG_PER_STEP * launch_steps / (mh_ms * 1e-3) / 1e9
+    # SURVEY §8d per-particle-step figures, for this workload's S and tile
+    S_, HW_ = cfg["sources"], cfg["tile"] * cfg["tile"]
+    b_alg = 24 * S_ + 8
+    f_alg = S_ * min(289, HW_) * 20 + HW_ * 10
+    achieved_gbs = b_alg * launch_steps / (mh_ms * 1e-3) / 1e9
     mh_rate = launch_steps / (mh_ms * 1e-3)
     traffic = None
     pmc = os.path.join(ROOT, "profiles", PMC_FILE)
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and args.workload == "c2" and not args.full_recompute:
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     out = {
-        "metric": "particle-steps/sec (4096 particles, 32x32 tile)",
+        "metric": ("particle-steps/sec (4096 particles, 32x32 tile)" if args.workload == "c2"
+                   else f"particle-steps/sec ({args.workload} workload)"),
         "value": value,
         "unit": "particle-steps/sec",
         "n_gpus": world,
@@ -223,27 +288,24 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (M71 prior + image model, seed 1000+rank)",
-        "config": {"workload": f"C2: {T} x {H}x{H} tile(s)/GPU, S={S}, N={Np}, "
-                               f"{K} MH iters per SMC step, systematic, rho=0.5",
-                   "tiles_per_gpu": T, "particles": Np, "tile": H, "sources": S,
-                   "mh_iters": K, "mode": "full" if args.full_recompute else "incremental",
-                   "parallelism": f"tile-sharded x{world}"},
+        "config": dict(cfg, mode="full" if args.full_recompute else "incremental",
+                       parallelism=f"tile-sharded x{world}"),
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "smcdet mh_sweep_kernel", "kernel_ms": mh_ms,
-                     "alg_bytes_per_particle_step": B_ALG_PER_STEP},
+                     "alg_bytes_per_particle_step": b_alg},
         "compute": {"bound": "valu", "mh_particle_steps_per_s": mh_rate,
-                    "alg_flop_per_particle_step": F_ALG_PER_STEP,
-                    "achieved_alg_tflops": mh_rate * F_ALG_PER_STEP / 1e12,
+                    "alg_flop_per_particle_step": f_alg,
+                    "achieved_alg_tflops": mh_rate * f_alg / 1e12,
                     "peak_fp32_tflops": FP32_PEAK_TFLOPS,
-                    "frac": mh_rate * F_ALG_PER_STEP / 1e12 / FP32_PEAK_TFLOPS},
+                    "frac": mh_rate * f_alg / 1e12 / FP32_PEAK_TFLOPS},
         "smc": {"temperature_min": float(s.temperature.min()),
                 "acc_rate": float(s.mutation_acc_rates.mean()),
                 "ess_mean": float(s.ess.mean())},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
         try:
-            out["cpu_baseline"] = cpu_baseline(args, image[:H, :H].cpu().numpy(),
+            out["cpu_baseline"] = cpu_baseline(args, cpu_tile.cpu().numpy(),
                                                args.cpu_baseline_seconds)
         except Exception as e:  # report, never fail the bench line on it
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
