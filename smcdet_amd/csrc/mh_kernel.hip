@@ -92,9 +92,9 @@ __device__ __forceinline__ void tn_cache(float mu, float isig, float lb, float u
 // (hn, wn, fn).  Wave-uniform (SGPR) values.
 struct Proposal {
   int j;
-  float h, w, f, lf;      // current values of source j
-  float hn, wn, fn, lfn;  // proposed values
-  float hast;             // log q(z|z') - log q(z'|z)
+  float h, w;         // current location of source j
+  float hn, wn, fn;   // proposed location and flux
+  float hast;         // log q(z|z') - log q(z'|z)
 };
 
 struct Dim {  // per-lane constants of the dimension this lane proposes
@@ -335,6 +335,7 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   // proposed flux, bdp = prior term, bhs = summed Hastings term
   float bmu = 0.f, bampo = 0.f, bampn = 0.f, bdp = 0.f, bhs = 0.f;
   int bfl = 0;
+  unsigned bmg = 1u;  // lane 3b+1: ceil(65536 / union-window width), for q / bw
   int bj = 0, batch_k0 = 0, batch_n = 0;
   uint64_t dirty = 0;
   auto compute_batch = [&](int k0) {
@@ -361,6 +362,12 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
       propose_lane<false>(mu, c_ph, c_lZ, u, dm, bx, bph, blZ, bhd, blf);
     bmu = mu;
     bfl = (int)(((unsigned)ifloor16(mu) & 0xffffu) | ((unsigned)ifloor16(bx) << 16));
+    {  // union-window width of the column anchors (meaningful in lane 3b+1)
+      const int f0 = ifloor16(mu), f1 = ifloor16(bx);
+      const int c0_ = max(min(f0, f1) - m.R, 0), c1_ = min(max(f0, f1) + m.R, m.W - 1);
+      const unsigned bw_ = (unsigned)max(c1_ - c0_ + 1, 1);
+      bmg = (65536u + bw_ - 1u) / bw_;
+    }
     // lane 3b+2 (flux): amplitudes, prior term (kernel.py:64-112 via
     // prior.py:220-226: the uniform location terms are constant in the box)
     // and the Hastings sum of the triple, in the per-iteration order
@@ -452,7 +459,7 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
 #ifdef SMCDET_TRACE
       tr_pos += npos;
 #endif
-      const unsigned magic = (65536u + (unsigned)bw - 1u) / (unsigned)bw;  // q/bw, q < 1024
+      const unsigned magic = (unsigned)readlane((int)bmg, 3 * b + 1);  // q/bw, q < 1024
       const bool same = (fh0 == fh1) && (fw0 == fw1);
       const int ao_h = fh0 - m.R - r0, ao_w = fw0 - m.R - c0;
       const int an_h = fh1 - m.R - r0, an_w = fw1 - m.R - c0;
