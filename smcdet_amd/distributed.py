@@ -108,15 +108,16 @@ class TileShardedSMC:
                                    self.rank, self.world_size, dst=dst, group=self.group)
 
 
-def gather_tile_results(local: dict, num_tiles: int, tiles_per_side: int, rank: int,
+def gather_tile_results(local: dict, num_tiles: int, tiles_per_side, rank: int,
                         world_size: int, dst: int = 0, group=None):
     """Gathers dicts of [T_local, ...] tensors from every rank into
-    [tiles_per_side, tiles_per_side, ...] tensors on `dst`.  Tensors travel as
+    [tiles_per_side, tiles_per_side, ...] tensors on `dst` ([num_tiles, ...]
+    when tiles_per_side is None: independent images).  Tensors travel as
     float32 (integer fields are exact below 2^24) through all_gather on the
     group's backend (RCCL for GPU tensors, gloo for CPU tensors)."""
+    lead = (num_tiles,) if tiles_per_side is None else (tiles_per_side, tiles_per_side)
     if world_size == 1:
-        return {k: v.reshape(tiles_per_side, tiles_per_side, *v.shape[1:])
-                for k, v in local.items()}
+        return {k: v.reshape(*lead, *v.shape[1:]) for k, v in local.items()}
     sizes = [shard_tiles(num_tiles, world_size, r) for r in range(world_size)]
     counts = [b - a for a, b in sizes]
     tmax = max(counts)
@@ -132,5 +133,37 @@ def gather_tile_results(local: dict, num_tiles: int, tiles_per_side: int, rank: 
         if rank == dst:
             full = torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
             full = full.reshape(num_tiles, *v.shape[1:]).to(dtype)
-            out[k] = full.reshape(tiles_per_side, tiles_per_side, *v.shape[1:])
+            out[k] = full.reshape(*lead, *v.shape[1:])
     return out if rank == dst else None
+
+
+class ShardedBatchSMC:
+    """BatchSMC (smcdet_amd.batch) over this rank's contiguous slice of B
+    independent images [B, H, W] (the m71 / m71synthetic cutouts, BASELINE
+    configs C4/C5): no collective until the end-of-run gather of the per-image
+    results (`gather_results`, [B, ...] on `dst`)."""
+
+    def __init__(self, images, Prior, ImageModel, MutationKernel, num_catalogs,
+                 ess_threshold_prop, resample_method, flux_detection_threshold, max_smc_iters,
+                 *, seed=None, device=None, group=None, **batch_kwargs):
+        from .batch import BatchSMC
+        self.rank, self.world_size = world()
+        self.group = group
+        self.num_images = images.shape[0]
+        self.start, self.stop = shard_tiles(self.num_images, self.world_size, self.rank)
+        if self.stop <= self.start:
+            raise ValueError(f"rank {self.rank} has no images ({self.num_images} images, "
+                             f"{self.world_size} ranks)")
+        seed = None if seed is None else int(seed) * 1000003 + self.rank
+        self.batch = BatchSMC(images[self.start:self.stop], Prior, ImageModel, MutationKernel,
+                              num_catalogs, ess_threshold_prop, resample_method,
+                              flux_detection_threshold, max_smc_iters, seed=seed, device=device,
+                              **batch_kwargs)
+
+    def run(self):
+        self.batch.run()
+        return self
+
+    def gather_results(self, dst=0):
+        return gather_tile_results(self.batch.results(), self.num_images, None, self.rank,
+                                   self.world_size, dst=dst, group=self.group)

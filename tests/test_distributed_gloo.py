@@ -75,6 +75,41 @@ def _worker(rank, world, port, num_tiles, tps, q):
         dist.destroy_process_group()
 
 
+def _worker_images(rank, world, port, num_images, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        a, b = shard_tiles(num_images, world, rank)
+        ids = torch.arange(a, b, dtype=torch.float32)
+        local = {"log_normalizing_constant": -ids, "counts": ids[:, None].repeat(1, 4),
+                 "num_iters": ids + 1}
+        out = gather_tile_results(local, num_images, None, rank, world, dst=0)
+        q.put(out if rank == 0 else None)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_independent_images_gloo():
+    world, num_images = 3, 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_images, args=(r, world, port, num_images, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full = next(g for g in got if g is not None)
+    ids = torch.arange(num_images, dtype=torch.float32)
+    assert torch.equal(full["log_normalizing_constant"], -ids)
+    assert full["counts"].shape == (num_images, 4)
+    assert torch.equal(full["num_iters"], ids + 1)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_gather_and_lockstep_gloo(world):
     num_tiles, tps = 9, 3
