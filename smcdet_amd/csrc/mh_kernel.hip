@@ -560,7 +560,9 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
       } else if (PAIRED && nslots <= 5) {
         dsum = same ? pairs(I2{}, One{}, Same{}) : pairs(I2{}, One{}, Win{});
       } else if (PAIRED) {
-        dsum = pairs(I3{}, Zero{}, Win{});
+        // 6 slots (both anchors moved): rare; the scalar form needs fewer
+        // registers than three packed pairs
+        dsum = slots(I8{}, Win{});
       } else if (nslots <= 3) {
         dsum = same ? slots(I3{}, Same{}) : slots(I3{}, Win{});
       } else if (nslots <= 5) {
