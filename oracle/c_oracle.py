@@ -22,7 +22,8 @@ class _Model(ctypes.Structure):
 
 
 class _Prior(ctypes.Structure):
-    _fields_ = [("kind", ctypes.c_int), ("alpha", ctypes.c_double)]
+    _fields_ = [("kind", ctypes.c_int)] + [(k, ctypes.c_double) for k in (
+        "alpha", "lower", "loc_low", "loc_high_h", "loc_high_w")]
 
 
 class _MH(ctypes.Structure):
@@ -44,6 +45,7 @@ def lib():
             build()
         _lib = ctypes.CDLL(LIB)
         _lib.mh_oracle_sweep.restype = ctypes.c_int
+        _lib.mala_oracle_sweep.restype = ctypes.c_int
     return _lib
 
 
@@ -64,6 +66,10 @@ def _pack(model, prior, mh):
     p = _Prior()
     p.kind = 1 if isinstance(prior, O.M71PriorP) else 2
     p.alpha = float(np.float32(prior.flux_alpha))
+    p.lower = float(np.float32(prior.flux_lower if isinstance(prior, O.M71PriorP)
+                               else prior.flux_scale))
+    p.loc_low = float(np.float32(prior.loc_low))
+    p.loc_high_h, p.loc_high_w = (float(np.float32(v)) for v in prior.loc_high)
     h = _MH()
     h.K = mh.num_iters
     h.sl, h.sf = mh.locs_stdev, mh.fluxes_stdev
@@ -96,3 +102,35 @@ def mh_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mh, replay=No
                           P(f), P(t), T, N, S, P(rc_), P(ru), P(rf), P(ra),
                           ctypes.c_uint64(seed), threads, P(acc))
     return l, f, acc.reshape(nH, nW, N).mean(-1)
+
+
+def mala_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mala, replay=None, seed=0,
+               threads=0, record=False):
+    """SingleComponentMALA.run (smcdet/kernel.py:133-275) in C.  `mala` has
+    the MHParams fields with locs_stdev / fluxes_stdev = the step sizes.
+    Returns (locs, fluxes, acc_rate[nH,nW]) and, with record=True, also the
+    per-iteration gradients and proposals [K,nH,nW,N,3]."""
+    img = np.ascontiguousarray(tiled_image, dtype=np.float32)
+    nH, nW, N, S, _ = np.shape(locs)
+    T = nH * nW
+    K = mala.num_iters
+    c = np.ascontiguousarray(counts, dtype=np.float32)
+    l = np.array(locs, dtype=np.float32, order="C")
+    f = np.array(fluxes, dtype=np.float32, order="C")
+    t = np.ascontiguousarray(np.broadcast_to(np.asarray(tau, np.float32), (nH, nW)))
+    acc = np.zeros((T, N), np.uint8)
+    grads = np.zeros((K, nH, nW, N, 3), np.float32) if record else None
+    props = np.zeros((K, nH, nW, N, 3), np.float32) if record else None
+    m, p, h = _pack(model, prior, mala)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None else None  # noqa: E731
+    rc_ = ru = rf = ra = None
+    if replay is not None:
+        rc_ = np.ascontiguousarray(replay["comp"], dtype=np.int32)
+        ru = np.ascontiguousarray(replay["uloc"], dtype=np.float32)
+        rf = np.ascontiguousarray(replay["uflux"], dtype=np.float32)
+        ra = np.ascontiguousarray(replay["uacc"], dtype=np.float32)
+    lib().mala_oracle_sweep(ctypes.byref(m), ctypes.byref(p), ctypes.byref(h), P(img), P(c),
+                            P(l), P(f), P(t), T, N, S, P(rc_), P(ru), P(rf), P(ra),
+                            ctypes.c_uint64(seed), threads, P(acc), P(grads), P(props))
+    out = (l, f, acc.reshape(nH, nW, N).mean(-1))
+    return out + (grads, props) if record else out

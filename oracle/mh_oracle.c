@@ -1,7 +1,8 @@
 /*
  * mh_oracle.c — CPU ORACLE / CPU BASELINE (test infrastructure only).
  *
- * Plain-C float64 restatement of the reference's MH sweep with the reference's
+ * Plain-C float64 restatement of the reference's MH sweep (and, below, of its
+ * MALA sweep, smcdet/kernel.py:133-275) with the reference's
  * arithmetic: every proposal re-renders every source and re-evaluates every
  * pixel (smcdet/kernel.py:26-130 -> sampler.py:87-91 -> images.py:28-76 +
  * :159-175 / :85-102, prior.py:67-75/:183-189/:220-226,
@@ -31,6 +32,8 @@ typedef struct {
 typedef struct {
   int kind; /* 1 = M71Prior (truncated Pareto), 2 = ParetoStarPrior */
   double alpha;
+  double lower;                      /* flux substituted for f == 0 (prior.py:189, :226) */
+  double loc_low, loc_high_h, loc_high_w;
 } om_prior_t;
 
 typedef struct {
@@ -274,6 +277,237 @@ int mh_oracle_sweep(const om_model_t* m, const om_prior_t* pr, const om_mh_t* mh
     }
     free(h);
     free(rate);
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------------
+ * SingleComponentMALA.run (smcdet/kernel.py:133-275).
+ *
+ * The image log-likelihood, its gradient and the prior are float64 (the
+ * gradient analytic: d loglik / d rate per pixel times d rate / d (h, w, f)
+ * over the moved source's PSF window, as torch.autograd.grad computes it,
+ * kernel.py:160-166 / :190-197).  The proposal machinery is float32 in the
+ * reference's operation order (distributions.py:22-52 on torch float32
+ * tensors), because its saturation points decide outcomes: Normal.cdf
+ * saturates to exactly 0 or 1 a few sigma outside the box, the mass-in-box
+ * log becomes -FLT_MAX (nan_to_num), and the float32 sums of kernel.py:220-251
+ * then absorb the log target.  Location proposals clamped to the box's upper
+ * edge have log prior -inf (torch Uniform.log_prob is -inf at `high`).
+ * ---------------------------------------------------------------------- */
+static const float kFltMax = 3.4028234663852886e38f;
+
+static float cdf_f(float v, float mu, float rsig) {
+  return 0.5f * (1.0f + erff((v - mu) * rsig / 1.41421356237309504880f));
+}
+static float nan_to_num_f(float x) {
+  if (isnan(x)) return 0.0f;
+  if (isinf(x)) return x > 0 ? kFltMax : -kFltMax;
+  return x;
+}
+static float tn_logZ_f(float mu, float rsig, float lb, float ub) {
+  return nan_to_num_f(logf(cdf_f(ub, mu, rsig) - cdf_f(lb, mu, rsig)));
+}
+static float tn_sample_f(float mu, float sig, float rsig, float lb, float ub, float u) {
+  const float p = u < 1e-6f ? 1e-6f : (u > (float)(1.0 - 1e-6) ? (float)(1.0 - 1e-6) : u);
+  float pt = cdf_f(lb, mu, rsig) + p * expf(tn_logZ_f(mu, rsig, lb, ub));
+  pt = pt < 1e-6f ? 1e-6f : (pt > (float)(1.0 - 1e-6) ? (float)(1.0 - 1e-6) : pt);
+  float x = mu + sig * (float)erfinv_d(2.0f * pt - 1.0f) * 1.41421356237309504880f;
+  return x < lb ? lb : (x > ub ? ub : x);
+}
+/* Normal(mu, sig).log_prob(v) - log_prob_in_box, torch's operation order */
+static float tn_logprob_f(float v, float mu, float sig, float rsig, float lb, float ub) {
+  const float d = v - mu;
+  const float lp = -(d * d) / (2.0f * (sig * sig)) - logf(sig) -
+                   (float)0.91893853320467274178;
+  return lp - tn_logZ_f(mu, rsig, lb, ub);
+}
+
+/* d phi / d r2 of the normalised PSF */
+static double psf_dr2(const om_model_t* m, double r2) {
+  if (m->model == 1) {
+    const double t1 = exp(-r2 / (2 * m->s1)) / (2 * m->s1);
+    const double t2 = m->b * exp(-r2 / (2 * m->s2)) / (2 * m->s2);
+    const double t3 = m->p0 * 0.5 / m->sp * pow(1 + r2 / (m->beta * m->sp), -m->beta / 2 - 1);
+    return -(t1 + t2 + t3) / (1 + m->b + m->p0) / m->norm;
+  }
+  return -psf_value(m, r2) / (2 * m->psf_stdev * m->psf_stdev);
+}
+
+/* d (per-pixel log-likelihood) / d rate */
+static double dll_drate(const om_model_t* m, double x, double lam) {
+  const double d = x - lam;
+  if (m->model == 1) {
+    const double v = m->s0sq + m->eta * lam;
+    return d / v + m->eta * d * d / (2 * v * v) - m->eta / (2 * v);
+  }
+  if (lam > 50000.0) return d / lam + d * d / (2 * lam * lam) - 1 / (2 * lam);
+  return x / lam - 1;
+}
+
+/* gradient of log_target w.r.t. (h_j, w_j, f_j); rate excludes background */
+static void mala_grad(const om_model_t* m, const om_prior_t* pr, const float* x,
+                      const double* rate, double h, double w, double f, int active,
+                      double tau, double* g) {
+  const int H = m->H, W = m->W, R = m->R;
+  const int fh = (int)floor(h), fw = (int)floor(w);
+  double gh = 0, gw = 0, gf = 0;
+  for (int ph = fh - R; ph <= fh + R; ++ph)
+    for (int pw = fw - R; pw <= fw + R; ++pw) {
+      if (ph < 0 || ph >= H || pw < 0 || pw >= W) continue;
+      const double dh = ph + 0.5 - h, dw = pw + 0.5 - w, r2 = dh * dh + dw * dw;
+      const double e = dll_drate(m, x[ph * W + pw], rate[ph * W + pw] + m->bg) * m->g;
+      const double dp = psf_dr2(m, r2);
+      gf += e * psf_value(m, r2);
+      gh += e * f * dp * (-2 * dh);
+      gw += e * f * dp * (-2 * dw);
+    }
+  g[0] = tau * gh;
+  g[1] = tau * gw;
+  g[2] = tau * gf;
+  if (active) g[2] -= (pr->alpha + 1) / (f == 0 ? pr->lower : f);
+}
+
+/* the state-dependent part of Prior.log_prob (prior.py:67-75 + :183-189 /
+ * :220-226): -(alpha+1) log f per active source, the uniform location
+ * density's support (-inf at or beyond `high`; -inf * 0 = nan for masked
+ * sources) -- the count and normalising constants cancel in every ratio */
+static double log_prior_var(const om_prior_t* pr, const double* h, const double* w,
+                            const double* f, int S, double cnt) {
+  double lp = 0;
+  for (int s = 0; s < S; ++s) {
+    const double act = s < cnt ? 1.0 : 0.0;
+    const int in = h[s] >= pr->loc_low && h[s] < pr->loc_high_h && w[s] >= pr->loc_low &&
+                   w[s] < pr->loc_high_w;
+    lp += (in ? 0.0 : -INFINITY) * act;
+    lp += -(pr->alpha + 1) * log(f[s] == 0 ? pr->lower : f[s]) * act;
+  }
+  return lp;
+}
+
+/*
+ * One MALA sweep; arguments as mh_oracle_sweep (mh->sl / mh->sf are the
+ * location / flux step sizes).  grad_out (nullable) [K,T,N,3] receives the
+ * gradient at the current state w.r.t. the chosen source's (h, w, f) each
+ * iteration, prop_out (nullable) [K,T,N,3] the proposal.
+ */
+int mala_oracle_sweep(const om_model_t* m, const om_prior_t* pr, const om_mh_t* mh,
+                      const float* image, const float* counts, float* locs, float* fluxes,
+                      const float* tau, int T, int N, int S, const int32_t* comp,
+                      const float* uloc, const float* uflux, const float* uacc, uint64_t seed,
+                      int threads, uint8_t* acc_last, float* grad_out, float* prop_out) {
+  const int HW = m->H * m->W;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#endif
+#pragma omp parallel
+  {
+    double* h = malloc(sizeof(double) * S * 3);
+    double* w = h + S;
+    double* f = w + S;
+    double* rate = malloc(sizeof(double) * HW * 3);
+    double* rate_p = rate + HW;
+    double* lgx = rate_p + HW;
+    const float sl = (float)mh->sl, sf = (float)mh->sf;
+    const float rsl = 1.0f / sl, rsf = 1.0f / sf;
+    const float cl = 0.5f * (sl * sl), cf = 0.5f * (sf * sf);
+    const float lbh = (float)mh->lb_h, lbw = (float)mh->lb_w, ubh = (float)mh->ub_h;
+    const float ubw = (float)mh->ub_w, lbf = (float)mh->lb_f, ubf = (float)mh->ub_f;
+#pragma omp for schedule(dynamic, 4)
+    for (long pid = 0; pid < (long)T * N; ++pid) {
+      const int t = (int)(pid / N);
+      const float* x = image + (size_t)t * HW;
+      for (int p = 0; p < HW; ++p) lgx[p] = lgamma((double)x[p] + 1.0);
+      for (int s = 0; s < S; ++s) {
+        h[s] = locs[(pid * S + s) * 2 + 0];
+        w[s] = locs[(pid * S + s) * 2 + 1];
+        f[s] = fluxes[pid * S + s];
+      }
+      const double cnt = counts[pid];
+      const double tk = tau[t];
+      uint64_t st = seed ^ (0x5A5A5A5Aull * (uint64_t)(pid + 1));
+      double ll = loglik(m, x, h, w, f, S, rate, lgx);
+      int acc = 0;
+      for (int k = 0; k < mh->K; ++k) {
+        int j;
+        float uh, uw, uf, ua;
+        const size_t r = ((size_t)k * T + t) * N + (pid % N);
+        if (comp) {
+          j = comp[r];
+          uh = uloc[r * 2];
+          uw = uloc[r * 2 + 1];
+          uf = uflux[r];
+          ua = uacc[r];
+        } else {
+          j = (int)(urand(&st) * S);
+          if (j >= S) j = S - 1;
+          uh = (float)urand(&st);
+          uw = (float)urand(&st);
+          uf = (float)urand(&st);
+          ua = (float)urand(&st);
+        }
+        const int active = j < cnt;
+        const double lp = log_prior_var(pr, h, w, f, S, cnt);
+        const float lt = (float)(lp + tk * ll);
+        double g[3];
+        mala_grad(m, pr, x, rate, h[j], w[j], f[j], active, tk, g);
+        const float oh = (float)h[j], ow = (float)w[j], of = (float)f[j];
+        /* kernel.py:168-190: mean = x + 0.5 step^2 grad */
+        const float mh_ = oh + cl * (float)g[0], mw_ = ow + cl * (float)g[1];
+        const float mf_ = of + cf * (float)g[2];
+        const float nh = tn_sample_f(mh_, sl, rsl, lbh, ubh, uh);
+        const float nw = tn_sample_f(mw_, sl, rsl, lbw, ubw, uw);
+        const float nf = tn_sample_f(mf_, sf, rsf, lbf, ubf, uf);
+        if (grad_out)
+          for (int d = 0; d < 3; ++d) grad_out[r * 3 + d] = (float)g[d];
+        if (prop_out) {
+          prop_out[r * 3 + 0] = nh;
+          prop_out[r * 3 + 1] = nw;
+          prop_out[r * 3 + 2] = nf;
+        }
+        /* denominator q(z'|z) (kernel.py:238-251) */
+        const float dq_l = tn_logprob_f(nh, mh_, sl, rsl, lbh, ubh) +
+                           tn_logprob_f(nw, mw_, sl, rsl, lbw, ubw);
+        const float dq_f = tn_logprob_f(nf, mf_, sf, rsf, lbf, ubf);
+        h[j] = nh;
+        w[j] = nw;
+        f[j] = nf;
+        const double nll = loglik(m, x, h, w, f, S, rate_p, lgx);
+        const double nlp = log_prior_var(pr, h, w, f, S, cnt);
+        const float nlt = (float)(nlp + tk * nll);
+        double gp[3];
+        mala_grad(m, pr, x, rate_p, h[j], w[j], f[j], active, tk, gp);
+        /* numerator q(z|z') (kernel.py:199-224) */
+        const float rh = nh + cl * (float)gp[0], rw = nw + cl * (float)gp[1];
+        const float rf = nf + cf * (float)gp[2];
+        const float nq_l = tn_logprob_f(oh, rh, sl, rsl, lbh, ubh) +
+                           tn_logprob_f(ow, rw, sl, rsl, lbw, ubw);
+        const float nq_f = tn_logprob_f(of, rf, sf, rsf, lbf, ubf);
+        const float num = (nlt + nq_l) + nq_f;
+        const float den = (lt + dq_l) + dq_f;
+        float alpha = expf(num - den);
+        if (alpha > 1.0f) alpha = 1.0f;
+        acc = ua <= alpha; /* nan -> reject */
+        if (acc) {
+          ll = nll;
+          double* tmp = rate;
+          rate = rate_p;
+          rate_p = tmp;
+        } else {
+          h[j] = oh;
+          w[j] = ow;
+          f[j] = of;
+        }
+      }
+      for (int s = 0; s < S; ++s) {
+        locs[(pid * S + s) * 2 + 0] = (float)h[s];
+        locs[(pid * S + s) * 2 + 1] = (float)w[s];
+        fluxes[pid * S + s] = (float)f[s];
+      }
+      if (acc_last) acc_last[pid] = (uint8_t)acc;
+    }
+    free(h);
+    free(rate < rate_p ? rate : rate_p);
   }
   return 0;
 }

@@ -88,6 +88,24 @@ def mh_fixture_setup(name):
 MH_FIXTURES = ["mh_m71_8x8", "mh_m71_32x32", "mh_m71_tiles", "mh_basic_16x16"]
 
 
+def mala_fixture_setup(name):
+    """tests/golden/make_golden.py gen_mala: the MH fixtures' geometries,
+    with SingleComponentMALA(K, locs_step, fluxes_step, fluxes_min, fluxes_max)."""
+    if name in ("mala_m71_8x8", "mala_m71_8x8_tau1"):
+        return 8, o_m71_model(8), o_m71_prior(8, 4, 4), o_m71_mh(20)
+    if name == "mala_m71_32x32":
+        return 32, o_m71_model(32), o_m71_prior(32, 10, 10), o_m71_mh(10)
+    if name == "mala_m71_tiles":
+        return 8, o_m71_model(8), o_m71_prior(8, 3, 3), o_m71_mh(10)
+    if name == "mala_basic_16x16":
+        return 16, o_basic_model(16), o_basic_prior(16, 3, 3), o_basic_mh(20)
+    raise KeyError(name)
+
+
+MALA_FIXTURES = ["mala_m71_8x8", "mala_m71_8x8_tau1", "mala_m71_32x32", "mala_m71_tiles",
+                 "mala_basic_16x16"]
+
+
 # ---- product-side constructors (smcdet_amd) -------------------------------
 def p_m71_model(H):
     from smcdet_amd.images import M71ImageModel

@@ -29,7 +29,7 @@ sys.path.insert(0, REF)
 
 from smcdet.distributions import TruncatedDiagonalMVN, TruncatedPareto  # noqa: E402
 from smcdet.images import ImageModel, M71ImageModel, generate_images  # noqa: E402
-from smcdet.kernel import SingleComponentMH  # noqa: E402
+from smcdet.kernel import SingleComponentMALA, SingleComponentMH  # noqa: E402
 from smcdet.prior import M71Prior, ParetoStarPrior  # noqa: E402
 from smcdet.sampler import SMCsampler  # noqa: E402
 
@@ -58,7 +58,8 @@ BASIC_FLUX_ALPHA = (-np.log(1 - 0.99)) / (
 
 
 class Recorder:
-    """Wraps torch.rand / Multinomial.sample / Tensor.multinomial; records draws."""
+    """Wraps torch.rand / torch.rand_like / Multinomial.sample /
+    Tensor.multinomial; records draws."""
 
     def __init__(self):
         self.draws = []  # list of (kind, np.ndarray)
@@ -68,6 +69,7 @@ class Recorder:
         self._rand = torch.rand
         self._ms = torch.distributions.Multinomial.sample
         self._tm = torch.Tensor.multinomial
+        self._rl = torch.rand_like
 
         def rand(*a, **k):
             out = rec._rand(*a, **k)
@@ -84,13 +86,20 @@ class Recorder:
             rec.draws.append(("multinomial", out.detach().cpu().numpy().copy()))
             return out
 
+        def rl(*a, **k):
+            out = rec._rl(*a, **k)
+            rec.draws.append(("rand_like", out.detach().cpu().numpy().copy()))
+            return out
+
         torch.rand = rand
+        torch.rand_like = rl
         torch.distributions.Multinomial.sample = ms
         torch.Tensor.multinomial = tm
         return self
 
     def __exit__(self, *exc):
         torch.rand = self._rand
+        torch.rand_like = self._rl
         torch.distributions.Multinomial.sample = self._ms
         torch.Tensor.multinomial = self._tm
         return False
@@ -394,6 +403,100 @@ def gen_mh():
     save("mh_basic_16x16.npz", **d)
 
 
+def run_mala_recorded(image, tile_dim, prior, model, mala, N, tau, seed):
+    """Runs SingleComponentMALA.run (smcdet/kernel.py:133-275) once with
+    recorded draws, gradients (torch.autograd.grad outputs) and proposals."""
+    torch.manual_seed(seed)
+    s = sampler_for(image, tile_dim, prior, model, mala, N)
+    s.initialize()
+    nt = s.num_tiles_per_side
+    temperature = torch.full((nt, nt), float(tau))
+    targets = []
+    orig = s.log_target
+
+    def log_target(data, counts, locs, fluxes, temperature):
+        v = orig(data, counts, locs, fluxes, temperature)
+        targets.append((np32(locs), np32(fluxes), np32(v)))
+        return v
+
+    grads = []
+    orig_grad = torch.autograd.grad
+
+    def grad(*a, **k):
+        out = orig_grad(*a, **k)
+        grads.append((np32(out[0]), np32(out[1])))
+        return out
+
+    locs0, fluxes0 = s.locs.clone(), s.fluxes.clone()
+    torch.autograd.grad = grad
+    try:
+        with Recorder() as rec:
+            locs1, fluxes1, acc = mala.run(s.tiled_image, s.counts, s.locs.clone(),
+                                           s.fluxes.clone(), temperature, log_target)
+    finally:
+        torch.autograd.grad = orig_grad
+    K = mala.num_iters
+    kinds = [k for k, _ in rec.draws]
+    assert kinds == ["mask", "rand", "rand", "rand_like"] * K, kinds[:8]
+    masks = np.stack([rec.draws[4 * i][1] for i in range(K)])
+    uloc = np.stack([rec.draws[4 * i + 1][1] for i in range(K)])
+    uflux = np.stack([rec.draws[4 * i + 2][1] for i in range(K)])
+    uacc = np.stack([rec.draws[4 * i + 3][1] for i in range(K)])
+    comp = masks.argmax(-1).astype(np.int32)  # [K,nt,nt,N]
+    j = comp[..., None]
+    def sel2(a, jj):
+        return np.take_along_axis(a, jj[..., None].repeat(2, -1), axis=-2)[..., 0, :]
+
+    def sel1(a, jj):
+        return np.take_along_axis(a, jj, axis=-1)[..., 0]
+
+    def triple(lc, fl, i):
+        return np.concatenate([sel2(lc, j[i]), sel1(fl, j[i])[..., None]], -1)
+
+    # two log_target / grad calls per iteration: current state, proposal
+    g_cur = np.stack([triple(*grads[2 * i], i) for i in range(K)])
+    g_prop = np.stack([triple(*grads[2 * i + 1], i) for i in range(K)])
+    prop = np.stack([triple(targets[2 * i + 1][0], targets[2 * i + 1][1], i) for i in range(K)])
+    lt_cur = np.stack([targets[2 * i][2] for i in range(K)])
+    lt_prop = np.stack([targets[2 * i + 1][2] for i in range(K)])
+    return dict(image=np32(s.image), counts=np32(s.counts), locs0=np32(locs0),
+                fluxes0=np32(fluxes0), tau=np.float32(tau), comp=comp,
+                uloc=sel2(uloc, j).astype(np.float32), uflux=sel1(uflux, j).astype(np.float32),
+                uacc=uacc.astype(np.float32), locs1=np32(locs1), fluxes1=np32(fluxes1),
+                acc=np32(acc), grad_cur=g_cur, grad_prop=g_prop, proposal=prop,
+                logtarget_cur=lt_cur, logtarget_prop=lt_prop,
+                locs_min=np32(mala.locs_min), locs_max=np32(mala.locs_max))
+
+
+def gen_mala():
+    # M71 8x8, S=4, N=32, K=20 (the MH fixture's geometry)
+    res = m71_truth_image(8, 41)
+    mala = SingleComponentMALA(20, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    d = run_mala_recorded(res[-1][0], 8, m71_prior(8, 4, 4), m71_model(8), mala, 32, 0.3, 151)
+    save("mala_m71_8x8.npz", **d)
+    # same image at tau = 1 (large gradients: proposal means leave the box)
+    mala = SingleComponentMALA(20, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    d = run_mala_recorded(res[-1][0], 8, m71_prior(8, 4, 4), m71_model(8), mala, 32, 1.0, 152)
+    save("mala_m71_8x8_tau1.npz", **d)
+    # M71 32x32 (C2 geometry), S=10, N=8, K=10
+    res = m71_truth_image(32, 42, counts_rate=0.003125, max_sources=10)
+    mala = SingleComponentMALA(10, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    d = run_mala_recorded(res[-1][0], 32, m71_prior(32, 10, 10), m71_model(32), mala, 8, 0.05,
+                          153)
+    save("mala_m71_32x32.npz", **d)
+    # 2x2 tiles of 8x8 (multi-tile indexing)
+    res = m71_truth_image(16, 43)
+    mala = SingleComponentMALA(10, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    d = run_mala_recorded(res[-1][0], 8, m71_prior(8, 3, 3), m71_model(8), mala, 8, 0.5, 154)
+    save("mala_m71_tiles.npz", **d)
+    # basic Poisson model 16x16, S=3, N=32, K=20
+    res = basic_truth_image(16, 44)
+    pr = basic_prior(16, 3, 3)
+    mala = SingleComponentMALA(20, 0.1, 100, pr.flux_scale, 1e6)
+    d = run_mala_recorded(res[-1][0], 16, pr, basic_model(16), mala, 32, 0.5, 155)
+    save("mala_basic_16x16.npz", **d)
+
+
 def gen_smc_steps():
     out = {}
     # temper: loglik vectors from prior states of a 32x32 tile, several tau
@@ -635,6 +738,9 @@ if __name__ == "__main__":
         gen_mh()
         gen_smc_steps()
         gen_smc_replay()
+        gen_mala()
+    elif what == "mala":
+        gen_mala()
     elif what == "cssmc":
         n = int(sys.argv[2]) if len(sys.argv) > 2 else 16
         gen_cssmc(list(range(n)))

@@ -4,7 +4,8 @@ import numpy as np
 import pytest
 
 from oracle import smc_oracle as O
-from tests._params import (M71, MH_FIXTURES, golden, mh_fixture_setup, o_basic_model,
+from tests._params import (M71, MALA_FIXTURES, MH_FIXTURES, golden, mala_fixture_setup,
+                           mh_fixture_setup, o_basic_model,
                            o_basic_prior, o_m71_mh, o_m71_model, o_m71_prior, tiles_of)
 
 
@@ -185,4 +186,33 @@ def test_c_oracle_mh_replay(name):
                                   prior, model, mh, replay=replay, threads=2)
     np.testing.assert_allclose(l, d["locs1"], rtol=0, atol=1e-5)
     np.testing.assert_allclose(f, d["fluxes1"], rtol=1e-6, atol=5e-4)
+    np.testing.assert_array_equal(acc.astype(np.float32), d["acc"])
+
+
+@pytest.mark.parametrize("name", MALA_FIXTURES)
+def test_c_oracle_mala_replay(name):
+    """The C MALA restatement (smcdet/kernel.py:133-275) replays the
+    reference's recorded draws: the same gradients as torch.autograd.grad, the
+    same proposals, accept decisions and final states.  The tau=1 and tile
+    fixtures include proposal means far outside the box (float32 mass-in-box
+    underflow) and proposals clamped to the box edge."""
+    from oracle import c_oracle
+    d = golden(name + ".npz")
+    td, model, prior, mala = mala_fixture_setup(name)
+    t = tiles_of(d["image"], td)
+    replay = {k: d[k] for k in ("comp", "uloc", "uflux", "uacc")}
+    l, f, acc, g, prop = c_oracle.mala_sweep(t, d["counts"], d["locs0"], d["fluxes0"],
+                                             float(d["tau"]), prior, model, mala, replay=replay,
+                                             threads=2, record=True)
+    gc = d["grad_cur"]
+    scale = np.abs(gc).max(axis=tuple(range(gc.ndim - 1)))
+    # iteration 0 (identical states): the analytic gradient vs autograd, to the
+    # reference's float32 summation error (~1e-7 x the summed |terms|)
+    np.testing.assert_array_less(np.abs(g[0] - gc[0]), 1e-4 * np.abs(gc[0]) + 1e-4 * scale + 1e-6)
+    # later iterations: states agree to float32 rounding, which the MALA drift
+    # (step^2/2 x gradient) can amplify to ~1e-3 relative before a proposal
+    np.testing.assert_array_less(np.abs(g - gc), 2e-2 * np.abs(gc) + 1e-4 * scale + 1e-6)
+    np.testing.assert_allclose(prop, d["proposal"], rtol=1e-6, atol=1e-3)
+    np.testing.assert_allclose(l, d["locs1"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(f, d["fluxes1"], rtol=1e-6, atol=1e-3)
     np.testing.assert_array_equal(acc.astype(np.float32), d["acc"])
