@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 5
+#define SMCDET_ABI_VERSION 6
 
 /* status codes */
 #define SMCDET_OK 0
@@ -186,6 +186,26 @@ int smcdet_mh_sweep(const smcdet_image_model_t* model,
                     uint64_t offset, const smcdet_mh_replay_t* replay,
                     uint32_t flags, float* loglik_out, float* acc_rate,
                     int32_t* acc_count, void* stream);
+
+/* SingleComponentMALA.run (smcdet/kernel.py:133-275), K iterations fused in
+ * one launch.  Arguments as smcdet_mh_sweep; mala->locs_stdev and
+ * mala->fluxes_stdev carry the step sizes (locs_step, fluxes_step,
+ * kernel.py:134-145).  The gradient of log_target w.r.t. the chosen source's
+ * (h, w, f) -- what torch.autograd.grad computes (kernel.py:160-166,
+ * :190-197) -- is evaluated analytically in-kernel over the source's PSF
+ * window.  Flags: SMCDET_MH_COMPONENT_BY_COUNT, SMCDET_MH_SKIP_DONE.
+ * The replay layout is smcdet_mh_replay_t's. */
+int smcdet_mala_sweep(const smcdet_image_model_t* model,
+                      const smcdet_prior_t* prior, const smcdet_mh_t* mala,
+                      const float* tiled_image, const float* temperature,
+                      int32_t T, int32_t N, int32_t S, const int64_t* ancestors,
+                      const float* counts_in, const float* locs_in,
+                      const float* fluxes_in, float* counts_out,
+                      float* locs_out, float* fluxes_out, const float* rate_in,
+                      float* rate_out, uint64_t seed,
+                      uint64_t offset, const smcdet_mh_replay_t* replay,
+                      uint32_t flags, float* loglik_out, float* acc_rate,
+                      int32_t* acc_count, void* stream);
 
 /* SMCsampler.temper (smcdet/sampler.py:93-125) on device: per tile, delta
  * solves exp(2 LSE(delta*l) - LSE(2 delta*l)) = ess_threshold on (0, 1-tau]

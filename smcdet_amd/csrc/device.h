@@ -126,6 +126,8 @@ enum RngTag : uint32_t {
   kTagResample = 0x52530000u,
   kTagNoise = 0x4e530000u,
   kTagStrata = 0x43530000u,
+  kTagMALA0 = 0x4d4c0000u,
+  kTagMALA1 = 0x4d4c0001u,
 };
 
 // ---------------------------------------------------------------------------

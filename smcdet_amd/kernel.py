@@ -1,4 +1,5 @@
-"""Mutation kernel (drop-in for smcdet/kernel.py:7-130, SingleComponentMH).
+"""Mutation kernels (drop-ins for smcdet/kernel.py:7-130, SingleComponentMH,
+and smcdet/kernel.py:133-275, SingleComponentMALA).
 
 `SingleComponentMH.run(data, counts, locs, fluxes, temperature, log_target)`
 keeps the reference signature and return value `[locs, fluxes, acc_rate]`.
@@ -24,6 +25,8 @@ def _f32(x):
 
 
 class SingleComponentMH(object):
+    _entry = "smcdet_mh_sweep"
+
     def __init__(self, num_iters, locs_stdev, fluxes_stdev, fluxes_min, fluxes_max, *,
                  full_recompute=False):
         self.num_iters = num_iters
@@ -144,7 +147,7 @@ class SingleComponentMH(object):
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(torch.cuda.current_stream(dev))
-        _hip.check(_hip.lib().smcdet_mh_sweep(
+        _hip.check(getattr(_hip.lib(), self._entry)(
             _hip.ref(cm), _hip.ref(cp), _hip.ref(ch), _hip.ptr(data), _hip.ptr(temperature),
             T, N, S, anc_p, _hip.ptr(counts), _hip.ptr(locs), _hip.ptr(fluxes),
             _hip.ptr(counts_out), _hip.ptr(locs_out), _hip.ptr(fluxes_out),
@@ -152,7 +155,7 @@ class SingleComponentMH(object):
             _hip.ptr(self._rate_buffer(rate_out, "rate_out", T * N, data)),
             self.rng.seed, off,
             _hip.ref(rp) if rp is not None else None, flags, _hip.ptr(ll), _hip.ptr(acc),
-            _hip.ptr(acc_ws), _hip.stream_of(locs)), "smcdet_mh_sweep")
+            _hip.ptr(acc_ws), _hip.stream_of(locs)), self._entry)
         if ev is not None:
             e1.record(torch.cuda.current_stream(dev))
             ev.append((e0, e1))
@@ -160,3 +163,37 @@ class SingleComponentMH(object):
         self.last_loglik = ll
         self.last_counts = counts_out if counts_out is not None else counts
         return [locs_out, fluxes_out, acc]
+
+
+class SingleComponentMALA(SingleComponentMH):
+    """smcdet/kernel.py:133-275: single-component Metropolis-adjusted Langevin
+    moves.  The chosen source's (location, flux) is proposed from truncated
+    normals centred at x + step^2/2 * grad log_target(x) and accepted with the
+    Metropolis-Hastings ratio including both truncated-proposal densities.
+    The reference obtains the gradient with torch.autograd.grad over the
+    whole image in every iteration; the fused gfx950 kernel
+    (smcdet_amd/csrc/mala_kernel.hip) evaluates it analytically over the
+    moved source's PSF window.  `run` has SingleComponentMH.run's signature
+    and return value."""
+    _entry = "smcdet_mala_sweep"
+
+    def __init__(self, num_iters, locs_step, fluxes_step, fluxes_min, fluxes_max):
+        super().__init__(num_iters, locs_step, fluxes_step, fluxes_min, fluxes_max)
+        self.locs_step = torch.tensor(locs_step)
+        self.fluxes_step = torch.tensor(fluxes_step)
+
+    @property
+    def locs_stdev(self):  # the C ABI's proposal-scale fields carry the steps
+        return self.locs_step
+
+    @locs_stdev.setter
+    def locs_stdev(self, v):
+        self.locs_step = torch.as_tensor(v)
+
+    @property
+    def fluxes_stdev(self):
+        return self.fluxes_step
+
+    @fluxes_stdev.setter
+    def fluxes_stdev(self, v):
+        self.fluxes_step = torch.as_tensor(v)

@@ -157,3 +157,20 @@ def p_mh_fixture_setup(name, **kw):
     if name == "mh_basic_16x16":
         return 16, p_basic_model(16), p_basic_prior(16, 3, 3), p_basic_mh(20, **kw)
     raise KeyError(name)
+
+
+def p_mala_fixture_setup(name):
+    from smcdet_amd.kernel import SingleComponentMALA
+    if name in ("mala_m71_8x8", "mala_m71_8x8_tau1"):
+        K, H, S = 20, 8, 4
+    elif name == "mala_m71_32x32":
+        K, H, S = 10, 32, 10
+    elif name == "mala_m71_tiles":
+        K, H, S = 10, 8, 3
+    elif name == "mala_basic_16x16":
+        return (16, p_basic_model(16), p_basic_prior(16, 3, 3),
+                SingleComponentMALA(20, 0.1, 100, BASIC_FLUX_SCALE * 0.9, 1e6))
+    else:
+        raise KeyError(name)
+    return (H, p_m71_model(H), p_m71_prior(H, S, S),
+            SingleComponentMALA(K, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"]))
