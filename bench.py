@@ -66,14 +66,25 @@ def parse():
     ap.add_argument("--mh-iters", type=int, default=100)
     ap.add_argument("--tiles-per-gpu", type=int, default=1)
     ap.add_argument("--full-recompute", action="store_true")
+    # mutation kernel: SingleComponentMH (the headline) or SingleComponentMALA
+    # (smcdet/kernel.py:133-275) on the same workload, as an extra line
+    ap.add_argument("--kernel", choices=["mh", "mala"], default="mh")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
 
+def mutation_kernel(args, K, full_recompute=False):
+    from smcdet_amd.kernel import SingleComponentMALA, SingleComponentMH
+    p = M71
+    if args.kernel == "mala":
+        return SingleComponentMALA(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"])
+    return SingleComponentMH(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"],
+                             full_recompute=full_recompute)
+
+
 def make_models(H, S):
     from smcdet_amd.images import M71ImageModel
-    from smcdet_amd.kernel import SingleComponentMH
     from smcdet_amd.prior import M71Prior
     p = M71
     model = M71ImageModel(image_height=H, image_width=H, background=p["background"],
@@ -86,7 +97,7 @@ def make_models(H, S):
     truth = M71Prior(min_objects=0, max_objects=100, counts_rate=COUNTS_RATE_C2, image_height=H,
                      image_width=H, flux_alpha=p["flux_alpha"],
                      flux_lower=p["flux_detection_threshold"], flux_upper=p["flux_upper"], pad=4)
-    return model, prior, truth, SingleComponentMH
+    return model, prior, truth
 
 
 def synthetic_image(model, truth, H, tiles_per_side, seed, dev, max_sources):
@@ -127,12 +138,13 @@ def cpu_baseline(args, image_tile, seconds):
     counts = np.full((1, 1, n), S, np.float32)
     img = image_tile.reshape(1, 1, H, H)
     c_oracle.lib()
+    sweep = c_oracle.mala_sweep if args.kernel == "mala" else c_oracle.mh_sweep
     # calibrate K so the timed sample takes ~`seconds`
     K = 2
     while True:
         mh = O.MHParams(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"])
         t0 = time.perf_counter()
-        c_oracle.mh_sweep(img, counts, locs, fl, 0.3, prior, model, mh, seed=1, threads=threads)
+        sweep(img, counts, locs, fl, 0.3, prior, model, mh, seed=1, threads=threads)
         dt = time.perf_counter() - t0
         if dt > seconds / 4 or K >= 4096:
             break
@@ -140,11 +152,12 @@ def cpu_baseline(args, image_tile, seconds):
     K = max(1, int(K * seconds / max(dt, 1e-6)))
     mh = O.MHParams(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"])
     t0 = time.perf_counter()
-    c_oracle.mh_sweep(img, counts, locs, fl, 0.3, prior, model, mh, seed=2, threads=threads)
+    sweep(img, counts, locs, fl, 0.3, prior, model, mh, seed=2, threads=threads)
     dt = time.perf_counter() - t0
     return {"value": n * K / dt, "unit": "particle-steps/sec", "cores": threads, "kind": "port",
-            "sample": f"oracle/mh_oracle.c float64 full re-render, {n} particles x {K} MH "
-                      f"iterations, {H}x{H} tile, S={S}, tau=0.3 ({dt:.1f} s)"}
+            "sample": f"oracle/mh_oracle.c float64 full re-render, {n} particles x {K} "
+                      f"{args.kernel.upper()} iterations, {H}x{H} tile, S={S}, tau=0.3 "
+                      f"({dt:.1f} s)"}
 
 
 def build_sampler(args, dev, rank):
@@ -154,21 +167,20 @@ def build_sampler(args, dev, rank):
     if args.workload == "c2":
         H, S, Np, K = args.tile, args.sources, args.particles, args.mh_iters
         tps = int(round(args.tiles_per_gpu ** 0.5))
-        model, prior, truth, MH = make_models(H, S)
+        model, prior, truth = make_models(H, S)
         image = synthetic_image(model, truth, H, tps, 1000 + rank, dev, max_sources=S)
-        mh = MH(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"], full_recompute=args.full_recompute)
+        mh = mutation_kernel(args, K, args.full_recompute)
         s = SMCsampler(image, H, prior, model, mh, Np, 0.5, "systematic",
                        p["flux_detection_threshold"], 10 ** 9, print_every=10 ** 9,
                        seed=12345 + rank, device=dev)
         T = tps * tps
         return s, mh, T * Np * K, image[:H, :H], dict(
-            workload=f"C2: {T} x {H}x{H} tile(s)/GPU, S={S}, N={Np}, {K} MH iters per SMC step, "
-                     "systematic, rho=0.5", tiles_per_gpu=T, particles=Np, tile=H, sources=S,
-            mh_iters=K)
+            workload=f"C2: {T} x {H}x{H} tile(s)/GPU, S={S}, N={Np}, {K} {args.kernel.upper()} "
+                     "iters per SMC step, systematic, rho=0.5", tiles_per_gpu=T, particles=Np,
+            tile=H, sources=S, mh_iters=K, kernel=args.kernel)
     # 8x8 M71 tiles at the real M71 source density (experiments/m71synthetic/
     # generate_images.py:27-67: truth from M71Prior(0, 100))
     from smcdet_amd.images import M71ImageModel
-    from smcdet_amd.kernel import SingleComponentMH
     from smcdet_amd.prior import M71Prior
     H, K, B = 8, args.mh_iters, max(1, args.tiles_per_gpu)
     model = M71ImageModel(image_height=H, image_width=H, background=p["background"],
@@ -181,7 +193,7 @@ def build_sampler(args, dev, rank):
     torch.manual_seed(2000 + rank)
     c, l, f = truth.sample(num_catalogs=B, device=dev)
     images = model.sample(l, f)[0, 0].permute(2, 0, 1).contiguous()       # [B, 8, 8]
-    mh = SingleComponentMH(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"])
+    mh = mutation_kernel(args, K)
     if args.workload == "c4":
         S, Np = 10, 4096
         prior = M71Prior(min_objects=S, max_objects=S, counts_rate=M71_COUNTS_RATE,
@@ -193,7 +205,7 @@ def build_sampler(args, dev, rank):
         return s, mh, B * Np * K, images[0], dict(
             workload=f"C4: {B} x 8x8 M71 tiles/GPU (batched), S={S}, N={Np}, {K} MH iters per "
                      "SMC step, systematic, rho=0.5", tiles_per_gpu=B, particles=Np, tile=H,
-            sources=S, mh_iters=K)
+            sources=S, mh_iters=K, kernel=args.kernel)
     from smcdet_amd.cssmc import CountStratifiedSMC
     smax, Np = 6, 8192
     prior = M71Prior(min_objects=0, max_objects=smax, counts_rate=M71_COUNTS_RATE,
@@ -207,7 +219,7 @@ def build_sampler(args, dev, rank):
         workload=f"C5: CS-SMC over {B} x 8x8 M71 tiles/GPU, counts 0..{smax} "
                  f"({NS} strata as tiles, S={smax}), N={Np} per count, {K} MH iters per SMC step, "
                  "systematic, rho=0.5", tiles_per_gpu=B, particles=Np * NS, tile=H, sources=smax,
-        mh_iters=K)
+        mh_iters=K, kernel=args.kernel)
 
 
 def main():
@@ -265,18 +277,25 @@ def main():
     S_, HW_ = cfg["sources"], cfg["tile"] * cfg["tile"]
     b_alg = 24 * S_ + 8
     f_alg = S_ * min(289, HW_) * 20 + HW_ * 10
+    if args.kernel == "mala":
+        # a MALA step needs the log target at the proposal and the gradient at
+        # the current state and at the proposal, each an adjoint sweep costing
+        # about one forward render: 3 x the MH figure
+        f_alg *= 3
     achieved_gbs = b_alg * launch_steps / (mh_ms * 1e-3) / 1e9
     mh_rate = launch_steps / (mh_ms * 1e-3)
     traffic = None
     pmc = os.path.join(ROOT, "profiles", PMC_FILE)
-    if os.path.exists(pmc) and args.workload == "c2" and not args.full_recompute:
+    if (os.path.exists(pmc) and args.workload == "c2" and not args.full_recompute
+            and args.kernel == "mh"):
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     out = {
-        "metric": ("particle-steps/sec (4096 particles, 32x32 tile)" if args.workload == "c2"
-                   else f"particle-steps/sec ({args.workload} workload)"),
+        "metric": ("particle-steps/sec (4096 particles, 32x32 tile)"
+                   if args.workload == "c2" and args.kernel == "mh"
+                   else f"particle-steps/sec ({args.workload} workload, {args.kernel})"),
         "value": value,
         "unit": "particle-steps/sec",
         "n_gpus": world,
@@ -292,7 +311,7 @@ def main():
                        parallelism=f"tile-sharded x{world}"),
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "smcdet mh_sweep_kernel", "kernel_ms": mh_ms,
+                     "kernel": f"smcdet {args.kernel}_sweep_kernel", "kernel_ms": mh_ms,
                      "alg_bytes_per_particle_step": b_alg},
         "compute": {"bound": "valu", "mh_particle_steps_per_s": mh_rate,
                     "alg_flop_per_particle_step": f_alg,

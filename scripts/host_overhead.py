@@ -20,7 +20,8 @@ from smcdet_amd.sampler import SMCsampler  # noqa: E402
 def main():
     dev = torch.device("cuda", 0)
     H, S, Np, K = 32, 10, 4096, 100
-    model, prior, truth, MH = bench.make_models(H, S)
+    model, prior, truth = bench.make_models(H, S)
+    from smcdet_amd.kernel import SingleComponentMH as MH
     image = bench.synthetic_image(model, truth, H, 1, 1000, dev, max_sources=S)
     mh = MH(K, 0.1, 2.5, bench.M71["flux_lower"], bench.M71["flux_upper"])
     s = SMCsampler(image, H, prior, model, mh, Np, 0.5, "systematic",

@@ -4,7 +4,8 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${OUT:-gpurun_out/prof}
+KRE=${KRE:-mh_sweep}  # kernel-name regex of the PMC passes
 mkdir -p $OUT
 B="bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-}"
 run() {  # $1 = name, rest = rocprofv3 args
@@ -19,9 +20,9 @@ if [ "${LIST:-0}" = "1" ]; then
 fi
 if [ "${TRACE:-1}" = "1" ]; then
   run trace --kernel-trace --stats
-  run fetch --pmc FETCH_SIZE --kernel-include-regex mh_sweep
-  run write --pmc WRITE_SIZE --kernel-include-regex mh_sweep
+  run fetch --pmc FETCH_SIZE --kernel-include-regex $KRE
+  run write --pmc WRITE_SIZE --kernel-include-regex $KRE
 fi
-if [ -n "${SQ:-}" ]; then run sq --pmc $SQ --kernel-include-regex mh_sweep; fi
-if [ -n "${SQ2:-}" ]; then run sq2 --pmc $SQ2 --kernel-include-regex mh_sweep; fi
-if [ -n "${SQ3:-}" ]; then run sq3 --pmc $SQ3 --kernel-include-regex mh_sweep; fi
+if [ -n "${SQ:-}" ]; then run sq --pmc $SQ --kernel-include-regex $KRE; fi
+if [ -n "${SQ2:-}" ]; then run sq2 --pmc $SQ2 --kernel-include-regex $KRE; fi
+if [ -n "${SQ3:-}" ]; then run sq3 --pmc $SQ3 --kernel-include-regex $KRE; fi

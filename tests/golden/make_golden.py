@@ -642,6 +642,14 @@ def gen_stats(which, seeds):
         model, tile, N = m71_model(8), 8, 1000
         # notebooks/smc.ipynb cell 7 resamples multinomially
         method = "systematic" if which == "m71" else "multinomial"
+    elif which == "m71_mala":
+        # SingleComponentMALA (smcdet/kernel.py:133-275): 8x8, S=4, N=500, K=50
+        res = m71_truth_image(8, 0)
+        img = res[-1][0]
+        pr = m71_prior(8, 4, 4)
+        mk = lambda: SingleComponentMALA(50, 0.1, 2.5, M71["flux_lower"],  # noqa: E731
+                                         M71["flux_upper"])
+        model, tile, N, method = m71_model(8), 8, 500, "systematic"
     else:
         raise ValueError(which)
     rows = []
@@ -671,8 +679,9 @@ def gen_stats(which, seeds):
                              s.posterior_mean_total_flux(s.pruned_fluxes).flatten()[0]),
                          runtime_s=dt))
         print(which, seed, rows[-1]["logZ"], rows[-1]["iters"], f"{dt:.1f}s", flush=True)
-    cfg = dict(which=which, tile=tile, N=N, S=pr.max_objects, K=100, method=method,
-               rho=0.5, torch_threads=torch.get_num_threads())
+    cfg = dict(which=which, tile=tile, N=N, S=pr.max_objects, K=mk().num_iters, method=method,
+               rho=0.5, torch_threads=torch.get_num_threads(),
+               kernel="mala" if which.endswith("mala") else "mh")
     path = os.path.join(HERE, f"stats_{which}.json")
     with open(path, "w") as f:
         json.dump(dict(config=cfg, image=img.numpy().tolist(), runs=rows), f)

@@ -5,6 +5,7 @@ SMCsampler.run() (CPU, float32) on a fixed image (make_golden.py stats):
   basic: 16x16 Poisson ImageModel + ParetoStarPrior(3,3), N=256, K=100, systematic
   m71:   8x8 M71ImageModel + M71Prior(10,10), N=1000, K=100, systematic
   m71_multinomial: the same with multinomial resampling (notebooks/smc.ipynb cell 7)
+  m71_mala: 8x8 M71 + M71Prior(4,4), N=500, SingleComponentMALA with K=50, systematic
 (make_golden.py passes the M71 flux_detection_threshold to both samplers.)
 Random streams cannot match torch's, so parity is distributional: mean log Z
 within 1% and within 3 pooled standard errors; non-final ESS = rho*N; final
@@ -36,6 +37,10 @@ def _run(which, cfg, image, seed, fused=True, persist=True):
     H, N, S = cfg["tile"], cfg["N"], cfg["S"]
     if which == "basic":
         prior, model, mh = p_basic_prior(H, S, S), p_basic_model(H), p_basic_mh(cfg["K"])
+    elif cfg.get("kernel") == "mala":
+        from smcdet_amd.kernel import SingleComponentMALA
+        prior, model = p_m71_prior(H, S, S), p_m71_model(H)
+        mh = SingleComponentMALA(cfg["K"], 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
     else:
         prior, model, mh = p_m71_prior(H, S, S), p_m71_model(H), p_m71_mh(cfg["K"])
     s = SMCsampler(image, H, prior, model, mh, N, cfg["rho"], cfg["method"],
@@ -61,7 +66,7 @@ def _se(a, b):
     return np.sqrt(np.var(a, ddof=1) / len(a) + np.var(b, ddof=1) / len(b))
 
 
-@pytest.mark.parametrize("which", ["basic", "m71", "m71_multinomial"])
+@pytest.mark.parametrize("which", ["basic", "m71", "m71_multinomial", "m71_mala"])
 def test_statistical_parity_vs_reference(which):
     if not os.path.exists(os.path.join(GOLDEN, f"stats_{which}.json")):
         pytest.skip(f"stats_{which}.json not generated")
@@ -76,7 +81,10 @@ def test_statistical_parity_vs_reference(which):
     se = _se(lz, lz_ref)
     diff = lz.mean() - lz_ref.mean()
     assert abs(diff) <= 3 * se, (which, lz.mean(), lz_ref.mean(), se)
-    assert abs(diff) <= 0.01 * abs(lz_ref.mean()), (which, lz.mean(), lz_ref.mean())
+    if cfg.get("kernel") != "mala":
+        # (SMC with MALA mixes poorly on this image: the reference's own log Z
+        # spreads over SD ~135 nats across seeds, so only the SE test applies)
+        assert abs(diff) <= 0.01 * abs(lz_ref.mean()), (which, lz.mean(), lz_ref.mean())
 
     # every non-final tempering step lands on ESS = rho*N (root of the ESS equation)
     for r in runs:
