@@ -322,6 +322,23 @@ def main():
                 "acc_rate": float(s.mutation_acc_rates.mean()),
                 "ess_mean": float(s.ess.mean())},
     }
+    # SURVEY §8d also asks for the wall time to temperature 1: one complete
+    # run() (initialise, SMC loop with its per-iteration stopping check, final
+    # resample, prune) on a fresh sampler, outside the timed region
+    s2, _, _, _, _ = build_sampler(args, dev, rank)
+    s2.print_every = 10 ** 9
+    s2.max_smc_iters = 500
+    import contextlib
+    import io
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with contextlib.redirect_stdout(io.StringIO()):
+        s2.run()
+    torch.cuda.synchronize()
+    run_s = time.perf_counter() - t0
+    out["smc"]["run_to_tau1"] = {"iterations": int(s2.iter), "wall_s": run_s,
+                                 "ms_per_iteration": run_s / max(int(s2.iter), 1) * 1e3,
+                                 "temperature_min": float(s2.temperature.min())}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
         try:
             out["cpu_baseline"] = cpu_baseline(args, cpu_tile.cpu().numpy(),

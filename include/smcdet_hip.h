@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 6
+#define SMCDET_ABI_VERSION 7
 
 /* status codes */
 #define SMCDET_OK 0
@@ -231,13 +231,20 @@ int smcdet_resample_index(const float* weights, int32_t T, int32_t N,
                           const float* u, int64_t* idx, void* stream);
 
 /* temper + update_weights (+ resample index when idx != null) fused: one
- * launch per SMC iteration instead of three.  flags: SMCDET_SMC_*. */
+ * launch per SMC iteration instead of three.  flags: SMCDET_SMC_*.
+ * finished_iter [T] (nullable, int32): set to `iter` when a tile's
+ * temperature reaches 1 while it holds a negative value (per-tile finishing
+ * iteration).  live [3] (nullable, int32, zero before the first call): after
+ * the call live[2] = the number of tiles still below temperature 1 (the
+ * reference's while condition, sampler.py:230); live[0..1] are workspace and
+ * left zero. */
 int smcdet_temper_reweight(const float* loglik, float* temperature,
                            float* temperature_prev, float* log_weights_unnorm,
                            float* weights, float* ess, float* log_norm_const,
                            int32_t T, int32_t N, double ess_threshold,
                            int32_t resample_method, uint64_t seed,
                            uint64_t offset, int64_t* idx, uint32_t flags,
+                           int32_t* finished_iter, int32_t iter, int32_t* live,
                            void* stream);
 
 /* Gather of the resampled state (smcdet/sampler.py:150-169). */

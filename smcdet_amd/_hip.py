@@ -74,7 +74,7 @@ _SIGS = {
     "smcdet_update_weights": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p], c_i),
     "smcdet_resample_index": ([c_p, c_i, c_i, c_i, c_u64, c_u64, c_p, c_p, c_p], c_i),
     "smcdet_temper_reweight": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_d, c_i, c_u64,
-                                c_u64, c_p, c_u32, c_p], c_i),
+                                c_u64, c_p, c_u32, c_p, c_i, c_p, c_p], c_i),
     "smcdet_gather": ([c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
     "smcdet_count_posterior": ([c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_u64, c_u64, c_p, c_p,
                                 c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),

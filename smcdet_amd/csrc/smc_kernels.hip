@@ -43,7 +43,26 @@ struct TileArgs {
   const float* u;            // replay uniforms or null
   int64_t* idx;              // [T,N]
   uint32_t smc_flags;        // SMCDET_SMC_*
+  int32_t* fin_iter;         // [T] SMC iteration a tile reached temperature 1 (-1: not yet) or null
+  int32_t iter;              // the caller's SMC iteration number
+  int32_t* live;             // [3] zeroed workspace: counter, ticket, tiles still below 1 (or null)
 };
+
+// end-of-temper bookkeeping, thread 0 of each tile: the iteration at which the
+// tile reached temperature 1, and (last tile, by ticket) the number of tiles
+// still below 1 -- the reference's while condition (sampler.py:230) without
+// extra launches; the counter and ticket are zero again afterwards
+__device__ __forceinline__ void tile_status(const TileArgs& a, int t, float tnew) {
+  if (a.fin_iter && tnew >= 1.0f && a.fin_iter[t] < 0) a.fin_iter[t] = a.iter;
+  if (a.live) {
+    atomicAdd(&a.live[0], tnew < 1.0f ? 1 : 0);
+    __threadfence();
+    if (atomicAdd(&a.live[1], 1) == a.T - 1) {
+      a.live[2] = atomicExch(&a.live[0], 0);
+      atomicExch(&a.live[1], 0);
+    }
+  }
+}
 
 // Workgroup reductions with ONE barrier each: wave DPP reductions -> per-wave
 // slots of a double-buffered LDS array -> every thread combines the kTW slots
@@ -244,7 +263,10 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
   // independent stopping: a finished tile stays as it is (uniform weights of
   // its final resampled population, identity ancestors, log Z unchanged)
   if ((a.smc_flags & SMCDET_SMC_FREEZE_DONE) && a.temperature[t] >= 1.0f) {
-    if ((a.flags & kDoTemper) && threadIdx.x == 0) a.temperature_prev[t] = a.temperature[t];
+    if ((a.flags & kDoTemper) && threadIdx.x == 0) {
+      a.temperature_prev[t] = a.temperature[t];
+      tile_status(a, t, a.temperature[t]);
+    }
     if (a.flags & kDoWeights) {
       for (int i = threadIdx.x; i < N; i += kTB) {
         a.log_w[(size_t)t * N + i] = 0.0f;
@@ -288,6 +310,7 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
     if (threadIdx.x == 0) {
       a.temperature_prev[t] = tau;
       a.temperature[t] = tnew;
+      tile_status(a, t, tnew);
     }
   }
 
@@ -732,7 +755,8 @@ int smcdet_temper_reweight(const float* loglik, float* temperature, float* tempe
                            float* log_weights_unnorm, float* weights, float* ess,
                            float* log_norm_const, int32_t T, int32_t N, double ess_threshold,
                            int32_t resample_method, uint64_t seed, uint64_t offset, int64_t* idx,
-                           uint32_t flags, void* stream) {
+                           uint32_t flags, int32_t* finished_iter, int32_t iter, int32_t* live,
+                           void* stream) {
   if (!loglik || !temperature || !temperature_prev || !log_weights_unnorm || !weights || !ess ||
       !log_norm_const)
     return set_error(SMCDET_EINVAL, "null buffer");
@@ -758,6 +782,9 @@ int smcdet_temper_reweight(const float* loglik, float* temperature, float* tempe
   a.offset = offset;
   a.idx = idx;
   a.smc_flags = flags;
+  a.fin_iter = finished_iter;
+  a.iter = iter;
+  a.live = live;
   return launch_tile(a, (hipStream_t)stream);
 }
 

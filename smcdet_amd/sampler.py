@@ -140,6 +140,7 @@ class SMCsampler(object):
         self._pending_idx = None
         # SMC iteration at which each tile reached temperature 1 (-1: not yet)
         self.iters_per_tile = torch.full((nH, nW), -1, device=self.device, dtype=torch.int32)
+        self._live_valid = False
 
     def log_target(self, data, counts, locs, fluxes, temperature):
         """sampler.py:87-91."""
@@ -174,6 +175,7 @@ class SMCsampler(object):
             "smcdet_temper")
         self.temperature_prev = prev_t
         self.temperature = new_t
+        self._live_valid = False
         self._mark_finished()
 
     def update_weights(self):
@@ -279,11 +281,21 @@ class SMCsampler(object):
             _hip.ptr(self.log_normalizing_constant), self._T, N, float(self.ess_threshold),
             self._method_code(), self.rng.seed, off, _hip.ptr(idx),
             _hip.SMCDET_SMC_FREEZE_DONE if self.stopping == "independent" else 0,
+            _hip.ptr(self.iters_per_tile), int(getattr(self, "iter", 0)), _hip.ptr(self._live_ws()),
             _hip.stream_of(new_t)), "smcdet_temper_reweight")
         self.temperature_prev = prev_t
         self.temperature = new_t
         self._pending_idx = idx
-        self._mark_finished()
+        self._live_valid = True
+
+    def _live_ws(self):
+        """[3] int32 zeroed once; the tile kernel leaves the number of tiles
+        below temperature 1 in [2] (smcdet_temper_reweight)."""
+        ws = getattr(self, "_live", None)
+        if ws is None or ws.device != self.temperature.device:
+            ws = torch.zeros(3, device=self.temperature.device, dtype=torch.int32)
+            self._live = ws
+        return ws
 
     def _mark_finished(self):
         it = getattr(self, "iters_per_tile", None)
@@ -318,7 +330,10 @@ class SMCsampler(object):
 
     def _keep_going(self):
         """sampler.py:230: continue while any tile has temperature < 1 (one
-        device->host read per SMC iteration)."""
+        device->host read per SMC iteration; after the fused temper launch the
+        count of unfinished tiles is already on the device)."""
+        if getattr(self, "_live_valid", False):
+            return int(self._live[2]) > 0
         return bool((self.temperature < 1).any())
 
     def run(self):
