@@ -134,3 +134,36 @@ def mala_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mala, repla
                             ctypes.c_uint64(seed), threads, P(acc), P(grads), P(props))
     out = (l, f, acc.reshape(nH, nW, N).mean(-1))
     return out + (grads, props) if record else out
+
+
+def mh_chain(tiled_image, counts, init_locs, init_fluxes, prior, model, mh, total, burnin, keep,
+             replay):
+    """MHsampler.run (smcdet/sampler.py:420-486): one MH chain per tile at
+    temperature 1, as total-1 single-iteration sweeps of the C restatement
+    under the recorded draws (replay [K, nH, nW] / [K, nH, nW, 2]).  Returns
+    the kept samples (sample m = state after iteration m-1, m >= burnin,
+    every keep-th) [nH,nW,M,S,2] / [nH,nW,M,S] and the accept flags [nH,nW,K]."""
+    import copy
+    nH, nW = np.shape(init_locs)[:2]
+    m1 = copy.copy(mh)
+    m1.num_iters = 1
+    l = np.asarray(init_locs, np.float32)[:, :, None].copy()
+    f = np.asarray(init_fluxes, np.float32)[:, :, None].copy()
+    c = np.asarray(counts, np.float32).reshape(nH, nW, 1)
+    kept_l, kept_f, acc = [], [], []
+    if burnin == 0:
+        kept_l.append(l[:, :, 0].copy())
+        kept_f.append(f[:, :, 0].copy())
+    for k in range(total - 1):
+        rp = {"comp": replay["comp"][k][None, ..., None],
+              "uloc": replay["uloc"][k][None, :, :, None],
+              "uflux": replay["uflux"][k][None, ..., None],
+              "uacc": replay["uacc"][k][None, ..., None]}
+        l, f, a = mh_sweep(tiled_image, c, l, f, 1.0, prior, model, m1, replay=rp, threads=1)
+        acc.append(a)
+        m = k + 1
+        if m >= burnin and (m - burnin) % keep == 0:
+            kept_l.append(l[:, :, 0].copy())
+            kept_f.append(f[:, :, 0].copy())
+    return (np.stack(kept_l, 2), np.stack(kept_f, 2),
+            np.stack(acc, -1).astype(np.int32))

@@ -31,7 +31,7 @@ from smcdet.distributions import TruncatedDiagonalMVN, TruncatedPareto  # noqa: 
 from smcdet.images import ImageModel, M71ImageModel, generate_images  # noqa: E402
 from smcdet.kernel import SingleComponentMALA, SingleComponentMH  # noqa: E402
 from smcdet.prior import M71Prior, ParetoStarPrior  # noqa: E402
-from smcdet.sampler import SMCsampler  # noqa: E402
+from smcdet.sampler import MHsampler, SMCsampler  # noqa: E402
 
 # M71 parameters (notebooks/smc.ipynb cell 2; full precision per SURVEY §8a)
 M71 = dict(
@@ -497,6 +497,56 @@ def gen_mala():
     save("mala_basic_16x16.npz", **d)
 
 
+def run_mcmc_recorded(image, tile_dim, prior, model, total, burnin, keep, seed):
+    """MHsampler (smcdet/sampler.py:301-493) with recorded draws: the initial
+    prior draw, then per iteration the component mask, the location and flux
+    uniforms of the truncated normals and the accept uniform."""
+    import contextlib
+    import io
+    torch.manual_seed(seed)
+    with Recorder() as rec:
+        s = MHsampler(image=image, tile_dim=tile_dim, Prior=prior, ImageModel=model,
+                      locs_stdev=0.1, fluxes_stdev=2.5,
+                      flux_detection_threshold=M71["flux_detection_threshold"],
+                      num_samples_total=total, num_samples_burnin=burnin, keep_every_k=keep,
+                      print_every=10 ** 9)
+        init_locs, init_fluxes = np32(s.locs[..., 0, :, :]), np32(s.fluxes[..., 0, :])
+        n_init = len(rec.draws)
+        with contextlib.redirect_stdout(io.StringIO()):
+            s.run()
+    draws = rec.draws[n_init:]
+    K = total - 1
+    kinds = [k for k, _ in draws]
+    assert kinds == ["mask", "rand", "rand", "rand"] * K, kinds[:8]
+    masks = np.stack([draws[4 * i][1] for i in range(K)])[..., 0, :]     # [K,nt,nt,S]
+    uloc = np.stack([draws[4 * i + 1][1] for i in range(K)])[..., 0, :, :]
+    uflux = np.stack([draws[4 * i + 2][1] for i in range(K)])[..., 0, :]
+    uacc = np.stack([draws[4 * i + 3][1] for i in range(K)])             # [K,nt,nt]
+    comp = masks.argmax(-1).astype(np.int32)
+    j = comp[..., None]
+    uloc_sel = np.take_along_axis(uloc, j[..., None].repeat(2, -1), axis=-2)[..., 0, :]
+    uflux_sel = np.take_along_axis(uflux, j, axis=-1)[..., 0]
+    return dict(image=np32(s.image), init_locs=init_locs, init_fluxes=init_fluxes,
+                comp=comp, uloc=uloc_sel.astype(np.float32),
+                uflux=uflux_sel.astype(np.float32), uacc=uacc.astype(np.float32),
+                total=np.int32(total), burnin=np.int32(burnin), keep=np.int32(keep),
+                counts=np32(s.counts), locs=np32(s.locs), fluxes=np32(s.fluxes),
+                accept=s.accept.numpy().astype(np.int32),
+                pruned_counts=s.pruned_counts.numpy().astype(np.int64),
+                pruned_locs=np32(s.pruned_locs), pruned_fluxes=np32(s.pruned_fluxes))
+
+
+def gen_mcmc():
+    # one 8x8 M71 tile, S=4: 300 samples, burn-in 100, every 2nd kept
+    res = m71_truth_image(8, 61)
+    d = run_mcmc_recorded(res[-1][0], 8, m71_prior(8, 4, 4), m71_model(8), 300, 100, 2, 161)
+    save("mcmc_m71_8x8.npz", **d)
+    # 16x16 image as 2x2 tiles of 8x8, S=3: 200 samples, burn-in 50, every 3rd
+    res = m71_truth_image(16, 62)
+    d = run_mcmc_recorded(res[-1][0], 8, m71_prior(8, 3, 3), m71_model(8), 200, 50, 3, 162)
+    save("mcmc_m71_tiles.npz", **d)
+
+
 def gen_smc_steps():
     out = {}
     # temper: loglik vectors from prior states of a 32x32 tile, several tau
@@ -748,8 +798,11 @@ if __name__ == "__main__":
         gen_smc_steps()
         gen_smc_replay()
         gen_mala()
+        gen_mcmc()
     elif what == "mala":
         gen_mala()
+    elif what == "mcmc":
+        gen_mcmc()
     elif what == "cssmc":
         n = int(sys.argv[2]) if len(sys.argv) > 2 else 16
         gen_cssmc(list(range(n)))

@@ -216,3 +216,22 @@ def test_c_oracle_mala_replay(name):
     np.testing.assert_allclose(l, d["locs1"], rtol=0, atol=2e-5)
     np.testing.assert_allclose(f, d["fluxes1"], rtol=1e-6, atol=1e-3)
     np.testing.assert_array_equal(acc.astype(np.float32), d["acc"])
+
+
+@pytest.mark.parametrize("name,td,S", [("mcmc_m71_8x8", 8, 4), ("mcmc_m71_tiles", 8, 3)])
+def test_c_oracle_mh_chain_replay(name, td, S):
+    """MHsampler (smcdet/sampler.py:301-493) = one single-component MH chain
+    per tile at temperature 1: the C restatement replays the reference's
+    recorded draws to the same kept samples and accept flags."""
+    from oracle import c_oracle
+    d = golden(name + ".npz")
+    t = tiles_of(d["image"], td)
+    nt = t.shape[0]
+    replay = {k: d[k] for k in ("comp", "uloc", "uflux", "uacc")}
+    l, f, acc = c_oracle.mh_chain(t, np.full((nt, nt), S, np.float32), d["init_locs"],
+                                  d["init_fluxes"], o_m71_prior(td, S, S), o_m71_model(td),
+                                  o_m71_mh(1), int(d["total"]), int(d["burnin"]), int(d["keep"]),
+                                  replay)
+    np.testing.assert_array_equal(acc, d["accept"])
+    np.testing.assert_allclose(l, d["locs"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(f, d["fluxes"], rtol=1e-6, atol=1e-4)
