@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 7
+#define SMCDET_ABI_VERSION 8
 
 /* status codes */
 #define SMCDET_OK 0
@@ -206,6 +206,31 @@ int smcdet_mala_sweep(const smcdet_image_model_t* model,
                       uint64_t offset, const smcdet_mh_replay_t* replay,
                       uint32_t flags, float* loglik_out, float* acc_rate,
                       int32_t* acc_count, void* stream);
+
+/* MHsampler.run (smcdet/sampler.py:301-486): one single-component MH chain
+ * per (tile, chain) at temperature 1 -- C chains per tile, T tiles (the
+ * reference runs C = 1).  locs_state [T,C,S,2] / fluxes_state [T,C,S] hold
+ * the chain state (the initial sample on the first call) and are updated in
+ * place; iterations [k_begin, k_end) of num_samples_total - 1 run in this
+ * call (chunked runs continue the same Philox streams).  Sample m is the
+ * state after iteration m-1 (sample 0 = the initial state); samples
+ * m >= num_samples_burnin with (m - burnin) % keep_every_k == 0 are written to
+ * locs_out [T,C,M,S,2] / fluxes_out [T,C,M,S], M = ceil((total - burnin) /
+ * keep), the reference's burn_thin_idx (sampler.py:339-341).  accept_out
+ * [T,C,total-1] int32 (nullable): the accept flag of every iteration.
+ * mh->locs_stdev / fluxes_stdev / bounds as in smcdet_mh_sweep (the
+ * reference takes the flux bounds from Prior.flux_lower/flux_upper).  Replay
+ * buffers: comp [total-1,T,C], uloc [total-1,T,C,2], uflux / uacc
+ * [total-1,T,C]. */
+int smcdet_mh_chain(const smcdet_image_model_t* model,
+                    const smcdet_prior_t* prior, const smcdet_mh_t* mh,
+                    const float* tiled_image, int32_t T, int32_t C, int32_t S,
+                    const float* counts, float* locs_state, float* fluxes_state,
+                    int32_t num_samples_total, int32_t num_samples_burnin,
+                    int32_t keep_every_k, int32_t k_begin, int32_t k_end,
+                    uint64_t seed, uint64_t offset,
+                    const smcdet_mh_replay_t* replay, float* locs_out,
+                    float* fluxes_out, int32_t* accept_out, void* stream);
 
 /* SMCsampler.temper (smcdet/sampler.py:93-125) on device: per tile, delta
  * solves exp(2 LSE(delta*l) - LSE(2 delta*l)) = ess_threshold on (0, 1-tau]

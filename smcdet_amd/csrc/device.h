@@ -128,6 +128,8 @@ enum RngTag : uint32_t {
   kTagStrata = 0x43530000u,
   kTagMALA0 = 0x4d4c0000u,
   kTagMALA1 = 0x4d4c0001u,
+  kTagChain0 = 0x43480000u,
+  kTagChain1 = 0x43480001u,
 };
 
 // ---------------------------------------------------------------------------

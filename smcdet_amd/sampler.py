@@ -411,3 +411,180 @@ class SMCsampler(object):
                 setattr(self, k, v.to(self.device) if torch.is_tensor(v) else v)
         self._fresh_loglik = st.get("loglik")
         self._pending_idx = None
+
+
+class MHsampler(object):
+    """Single-component MH chains (drop-in for smcdet/sampler.py:301-576).
+
+    The reference runs one chain per tile at temperature 1 for
+    num_samples_total - 1 iterations, stores every sample and keeps
+    burn_thin_idx = arange(burnin, total, keep_every_k) of them
+    (experiments/m71/run_mcmc.py:71-132: 50,000 samples per 8x8 image).  Here
+    all tiles' chains run in one gfx950 launch per `print_every` iterations
+    (smcdet_mh_chain), one wavefront per chain, and only the kept samples are
+    written.  `num_chains=C` (keyword) runs C independent chains per tile; their
+    kept samples are pooled along the sample axis (chain-major).
+
+    Attributes after run(), as the reference: counts [nH,nW,M] (= max_objects),
+    locs [nH,nW,M,S,2], fluxes [nH,nW,M,S], accept [nH,nW,total-1] (int32;
+    [nH,nW,C,total-1] for C > 1), pruned_counts / pruned_locs / pruned_fluxes,
+    has_run.  Before run(), locs / fluxes hold the initial state
+    [nH,nW,C,S,2] / [nH,nW,C,S] (the reference's sample 0); assigning them
+    sets the chains' starting points.
+    """
+
+    def __init__(self, image, tile_dim, Prior, ImageModel, locs_stdev, fluxes_stdev,
+                 flux_detection_threshold, num_samples_total, num_samples_burnin,
+                 keep_every_k: int = 1, print_every: int = 1000, *, num_chains=1, seed=None,
+                 device=None):
+        if device is None:
+            device = image.device if image.is_cuda else torch.device(
+                "cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        self.image = image.to(self.device, torch.float32)
+        self.image_dim = image.shape[0]
+        self.tile_dim = tile_dim
+        self.num_tiles_per_side = self.image_dim // self.tile_dim
+        if image.dim() == 4:  # pre-tiled [numH, numW, tile, tile] (see from_tiles)
+            self.tiled_image = self.image.contiguous()
+        else:
+            self.tiled_image = (self.image.unfold(0, self.tile_dim, self.tile_dim)
+                                .unfold(1, self.tile_dim, self.tile_dim).contiguous())
+        self.tiles_shape = tuple(self.tiled_image.shape[:2])
+
+        self.Prior = Prior
+        self.ImageModel = ImageModel
+        self.locs_stdev = torch.tensor(locs_stdev)
+        self.locs_min = Prior.loc_prior.low
+        self.locs_max = Prior.loc_prior.high
+        self.fluxes_stdev = torch.tensor(fluxes_stdev)
+        self.fluxes_min = torch.tensor(Prior.flux_lower)
+        self.fluxes_max = torch.tensor(Prior.flux_upper)
+        self.flux_detection_threshold = flux_detection_threshold
+
+        if num_samples_burnin >= num_samples_total:
+            raise ValueError("num_samples_burnin must be smaller than num_samples_total.")
+        self.num_samples_total = num_samples_total
+        self.num_samples_burnin = num_samples_burnin
+        self.keep_every_k = int(keep_every_k)
+        self.burn_thin_idx = torch.arange(num_samples_burnin, num_samples_total,
+                                          step=keep_every_k)
+        self.num_chains = int(num_chains)
+        self.rng = PhiloxStream(seed)
+
+        nH, nW = self.tiles_shape
+        C, S = self.num_chains, Prior.max_objects
+        # Prior.sample(stratify_by_count=True, num_catalogs_per_count=1), first
+        # catalog per chain (sampler.py:358-364); the target's counts are
+        # max_objects (:343-348)
+        _, l, f = Prior.sample_stratified(None, C, device=self.device, rng=self.rng,
+                                          tiles_shape=(nH, nW))
+        self.locs = l[:, :, :C].contiguous()
+        self.fluxes = f[:, :, :C].contiguous()
+        self.counts = torch.full((nH, nW, C), float(S), device=self.device)
+        self.accept = torch.zeros(nH, nW, num_samples_total - 1, dtype=torch.int32,
+                                  device=self.device)
+        self.print_every = print_every
+        self.has_run = False
+
+    @classmethod
+    def from_tiles(cls, tiles, *args, **kwargs):
+        """Chains for a pre-tiled [numH, numW, tile, tile] stack -- e.g. a batch
+        of independent cutouts [1, B, 8, 8] (run_mcmc.py's loop over images)."""
+        if tiles.dim() != 4 or tiles.shape[2] != tiles.shape[3]:
+            raise ValueError("tiles must be [numH, numW, tile, tile]")
+        return cls(tiles, tiles.shape[2], *args, **kwargs)
+
+    def log_target(self, data, counts, locs, fluxes):
+        """sampler.py:390-394."""
+        logprior = self.Prior.log_prob(counts, locs, fluxes)
+        loglik = self.ImageModel.loglikelihood(data, locs, fluxes)
+        return logprior + loglik
+
+    def prune(self, locs, fluxes):
+        """sampler.py:396-418 (the SMC sampler's rule, samples on axis 2)."""
+        return SMCsampler.prune(self, locs, fluxes)
+
+    def _cmh(self):
+        c = _hip.MHC()
+        c.num_iters = 1
+        c.locs_stdev = float(self.locs_stdev)
+        c.fluxes_stdev = float(self.fluxes_stdev)
+        c.fluxes_min = float(self.fluxes_min)
+        c.fluxes_max = float(self.fluxes_max)
+        lo = torch.as_tensor(self.locs_min).reshape(-1).cpu().float()
+        hi = torch.as_tensor(self.locs_max).reshape(-1).cpu().float()
+        c.locs_min_h, c.locs_min_w = float(lo[0]), float(lo[-1])
+        c.locs_max_h, c.locs_max_w = float(hi[0]), float(hi[-1])
+        return c
+
+    def run(self, *, replay=None):
+        """sampler.py:420-493.  replay = dict(comp [K,nH,nW(,C)], uloc
+        [K,nH,nW(,C),2], uflux / uacc [K,nH,nW(,C)]) replays recorded draws
+        (K = num_samples_total - 1)."""
+        nH, nW = self.tiles_shape
+        T, C, S = nH * nW, self.num_chains, self.Prior.max_objects
+        total, burnin, keep = self.num_samples_total, self.num_samples_burnin, self.keep_every_k
+        K = total - 1
+        M = (total - burnin + keep - 1) // keep
+        dev = self.device
+        ls = _hip.dev_f32(self.locs.reshape(nH, nW, C, S, 2).clone(), "locs")
+        fs = _hip.dev_f32(self.fluxes.reshape(nH, nW, C, S).clone(), "fluxes")
+        counts = _hip.dev_f32(self.counts.reshape(nH, nW, C), "counts")
+        lo = torch.empty(nH, nW, C, M, S, 2, device=dev)
+        fo = torch.empty(nH, nW, C, M, S, device=dev)
+        acc = torch.zeros(nH, nW, C, max(K, 1), dtype=torch.int32, device=dev)
+        rp, keepalive = None, []
+        if replay is not None:
+            rc = replay["comp"].to(device=dev, dtype=torch.int32).contiguous()
+            ru = [_hip.dev_f32(replay[k].to(dev), k) for k in ("uloc", "uflux", "uacc")]
+            keepalive = [rc] + ru
+            rp = _hip.ReplayC(_hip.ptr(rc).value, _hip.ptr(ru[0]).value, _hip.ptr(ru[1]).value,
+                              _hip.ptr(ru[2]).value)
+        off = self.rng.take(max(K, 1))
+        cm, cp, ch = self.ImageModel._cmodel(), self.Prior._cprior(), self._cmh()
+        chunk = max(1, int(self.print_every))
+        k0 = 0
+        while True:
+            k1 = min(K, k0 + chunk)
+            _hip.check(_hip.lib().smcdet_mh_chain(
+                _hip.ref(cm), _hip.ref(cp), _hip.ref(ch), _hip.ptr(self.tiled_image), T, C, S,
+                _hip.ptr(counts), _hip.ptr(ls), _hip.ptr(fs), total, burnin, keep, k0, k1,
+                self.rng.seed, off, _hip.ref(rp) if rp is not None else None, _hip.ptr(lo),
+                _hip.ptr(fo), _hip.ptr(acc), _hip.stream_of(ls)), "smcdet_mh_chain")
+            if k1 >= K:
+                break
+            k0 = k1
+            if k0 % chunk == 0:
+                mean_acc = acc[..., k0 - chunk:k0].float().mean().item()
+                print(f"iteration {k0}, acceptance rate in past {chunk} iters = {mean_acc:.2f}\n")
+        del keepalive
+        self.accept = acc[..., :K][:, :, 0] if C == 1 else acc[..., :K]
+        self.locs = lo.reshape(nH, nW, C * M, S, 2)
+        self.fluxes = fo.reshape(nH, nW, C * M, S)
+        self.counts = torch.full((nH, nW, C * M), float(S), device=dev)
+        self.pruned_counts, self.pruned_locs, self.pruned_fluxes = self.prune(self.locs,
+                                                                              self.fluxes)
+        self.has_run = True
+
+    def posterior_mean_count(self, counts):
+        return counts.float().mean(-1)
+
+    def posterior_mean_total_flux(self, fluxes):
+        return fluxes.sum(-1).mean()
+
+    @property
+    def posterior_predictive_total_observed_flux(self):
+        return self.ImageModel.sample(self.locs, self.fluxes).sum([-2, -3]).squeeze()
+
+    def summarize(self):
+        if self.has_run is False:
+            raise ValueError("Sampler hasn't been run yet.")
+        vals, cnts = self.pruned_counts.unique(return_counts=True)
+        print("posterior distribution of number of detectable stars within image boundary:")
+        print(vals.cpu())
+        print((cnts / self.pruned_counts.shape[-1]).round(decimals=3).cpu(), "\n")
+        print("posterior mean total intrinsic flux (including undetectable and/or in padding) =",
+              f"{self.posterior_mean_total_flux(self.fluxes).item()}\n")
+        print("posterior mean total intrinsic flux of detectable stars within image boundary =",
+              f"{self.posterior_mean_total_flux(self.pruned_fluxes).item()}\n")

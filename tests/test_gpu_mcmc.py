@@ -1,0 +1,112 @@
+"""GPU parity of MHsampler (smcdet/sampler.py:301-576; smcdet_amd/csrc/
+chain_kernel.hip through smcdet_mh_chain): replays of the reference's
+recorded chains (tests/golden/mcmc_*.npz, make_golden.py gen_mcmc) must keep
+the same samples with every accept decision equal; a C2-geometry chain under
+synthetic replayed draws must match the C oracle; chunked launches continue
+the chains."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import c_oracle
+from tests._params import (M71, golden, o_m71_mh, o_m71_model, o_m71_prior, p_m71_model,
+                           p_m71_prior, tiles_of)
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+def _sampler(image, td, S, d, **kw):
+    from smcdet_amd.sampler import MHsampler
+    s = MHsampler(torch.as_tensor(image, device=DEV), td, p_m71_prior(td, S, S), p_m71_model(td),
+                  0.1, 2.5, M71["flux_detection_threshold"], int(d["total"]), int(d["burnin"]),
+                  int(d["keep"]), **kw)
+    return s
+
+
+def _replay(d):
+    return {k: torch.as_tensor(d[k]) for k in ("comp", "uloc", "uflux", "uacc")}
+
+
+@pytest.mark.parametrize("name,td,S", [("mcmc_m71_8x8", 8, 4), ("mcmc_m71_tiles", 8, 3)])
+def test_mh_chain_replay_vs_reference(name, td, S):
+    d = golden(name + ".npz")
+    s = _sampler(d["image"], td, S, d, print_every=10 ** 9)
+    s.locs = torch.as_tensor(d["init_locs"][:, :, None], device=DEV)
+    s.fluxes = torch.as_tensor(d["init_fluxes"][:, :, None], device=DEV)
+    s.run(replay=_replay(d))
+    np.testing.assert_array_equal(N(s.accept), d["accept"])
+    np.testing.assert_allclose(N(s.locs), d["locs"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(N(s.fluxes), d["fluxes"], rtol=2e-6, atol=1e-3)
+    np.testing.assert_array_equal(N(s.counts), d["counts"])
+    np.testing.assert_array_equal(N(s.pruned_counts), d["pruned_counts"])
+    np.testing.assert_allclose(N(s.pruned_locs), d["pruned_locs"], rtol=0, atol=2e-5)
+    assert s.has_run
+
+
+def test_mh_chain_chunked_equals_single_launch():
+    """print_every chunks relaunch the kernel (re-rendered rate image, same
+    Philox streams): the same chain up to float32 near-ties."""
+    d = golden("mcmc_m71_8x8.npz")
+    outs = []
+    for pe in (10 ** 9, 37):
+        s = _sampler(d["image"], 8, 4, d, print_every=pe, seed=5)
+        s.run()
+        outs.append((N(s.locs), N(s.accept)))
+    assert (outs[0][1] == outs[1][1]).mean() > 0.97
+    np.testing.assert_allclose(outs[0][0][:, :, :20], outs[1][0][:, :, :20], rtol=0, atol=1e-3)
+
+
+def test_mh_chain_c2_vs_oracle():
+    """32x32 tile, S=10, 400 iterations under synthetic replayed draws: the
+    kernel's chain against the C restatement's (bench C2 geometry)."""
+    H, S, total, burnin, keep = 32, 10, 401, 1, 4
+    d = golden("mh_m71_32x32.npz")
+    img = tiles_of(d["image"], H)
+    rng = np.random.default_rng(7)
+    K = total - 1
+    rp = dict(comp=rng.integers(0, S, (K, 1, 1)).astype(np.int32),
+              uloc=rng.random((K, 1, 1, 2)).astype(np.float32),
+              uflux=rng.random((K, 1, 1)).astype(np.float32),
+              uacc=rng.random((K, 1, 1)).astype(np.float32))
+    init_l, init_f = d["locs0"][:, :, :1], d["fluxes0"][:, :, :1]
+    oprior = o_m71_prior(H, S, S)
+    ol, of_, oacc = c_oracle.mh_chain(img, np.full((1, 1), S, np.float32), init_l[:, :, 0],
+                                      init_f[:, :, 0], oprior, o_m71_model(H), o_m71_mh(1), total,
+                                      burnin, keep, rp)
+    from smcdet_amd.sampler import MHsampler
+    s = MHsampler(torch.as_tensor(d["image"], device=DEV), H, p_m71_prior(H, S, S),
+                  p_m71_model(H), 0.1, 2.5, M71["flux_detection_threshold"], total, burnin, keep,
+                  print_every=10 ** 9)
+    s.locs = torch.as_tensor(init_l, device=DEV)
+    s.fluxes = torch.as_tensor(init_f, device=DEV)
+    s.run(replay={k: torch.as_tensor(v) for k, v in rp.items()})
+    same = (N(s.accept) == oacc).mean()
+    assert same > 0.99, same
+    first = int(np.argmax(N(s.accept)[0, 0] != oacc[0, 0])) if same < 1 else K
+    m = max(0, (first - burnin) // keep)
+    np.testing.assert_allclose(N(s.locs)[:, :, :m], ol[:, :, :m], rtol=0, atol=1e-4)
+
+
+def test_mh_chain_many_chains_and_images():
+    """C chains x a batch of images in one launch: shapes, bounds, pooled
+    samples, and independent streams per chain."""
+    from smcdet_amd.sampler import MHsampler
+    d = golden("mcmc_m71_tiles.npz")
+    tiles = torch.as_tensor(tiles_of(d["image"], 8), device=DEV).reshape(1, 4, 8, 8)
+    s = MHsampler.from_tiles(tiles, p_m71_prior(8, 3, 3), p_m71_model(8), 0.1, 2.5,
+                             M71["flux_detection_threshold"], 1000, 500, 5, print_every=10 ** 9,
+                             num_chains=8, seed=3)
+    s.run()
+    assert tuple(s.locs.shape) == (1, 4, 8 * 100, 3, 2)
+    assert tuple(s.accept.shape) == (1, 4, 8, 999)
+    lc = N(s.locs)
+    assert lc.min() >= -4 and lc.max() < 12
+    per_chain = lc.reshape(1, 4, 8, 100, 3, 2)
+    assert not np.allclose(per_chain[:, :, 0], per_chain[:, :, 1])
+    assert 0.05 < float(s.accept.float().mean()) < 0.99
+    assert s.posterior_mean_count(s.pruned_counts).shape == (1, 4)
