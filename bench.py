@@ -57,7 +57,10 @@ def parse():
     # BASELINE.json configs[3] / [4] run as extra lines: batches of 8x8 M71
     # tiles (N=4096, S=10) and count-stratified SMC over 8x8 tiles (counts
     # 0..6, 8192 particles per count), per GPU.
-    ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2")
+    # mcmc: the reference's MCMC baseline (MHsampler, experiments/m71/
+    # run_mcmc.py: 8x8 M71 cutouts, S=10, 50,000 samples, burn-in 30,000,
+    # every 2nd kept), one chain per image, a batch of images per GPU
+    ap.add_argument("--workload", choices=["c2", "c4", "c5", "mcmc"], default="c2")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--particles", type=int, default=4096)
@@ -222,6 +225,65 @@ def build_sampler(args, dev, rank):
         mh_iters=K, kernel=args.kernel)
 
 
+def bench_mcmc(args, dev, rank, world):
+    """MHsampler over a batch of 8x8 M71 cutouts (one chain each): the whole
+    run() is timed, as run_mcmc.py:121-125 times it per image."""
+    from smcdet_amd.images import M71ImageModel
+    from smcdet_amd.prior import M71Prior
+    from smcdet_amd.sampler import MHsampler
+    p = M71
+    H, S, B = 8, 10, max(1, args.tiles_per_gpu)
+    total, burnin, keep = 50000, 30000, 2
+    model = M71ImageModel(image_height=H, image_width=H, background=p["background"],
+                          psf_radius=p["psf_radius"], adu_per_nmgy=p["adu_per_nmgy"],
+                          psf_params=p["psf_params"], noise_additive=p["noise_additive"],
+                          noise_multiplicative=p["noise_multiplicative"])
+    truth = M71Prior(min_objects=0, max_objects=100, counts_rate=M71_COUNTS_RATE, image_height=H,
+                     image_width=H, flux_alpha=p["flux_alpha"],
+                     flux_lower=p["flux_detection_threshold"], flux_upper=p["flux_upper"], pad=4)
+    prior = M71Prior(min_objects=S, max_objects=S, counts_rate=M71_COUNTS_RATE, image_height=H,
+                     image_width=H, flux_alpha=p["flux_alpha"], flux_lower=p["flux_lower"],
+                     flux_upper=p["flux_upper"], pad=4)
+    torch.manual_seed(2000 + rank)
+    c, l, f = truth.sample(num_catalogs=B, device=dev)
+    tiles = model.sample(l, f)[0, 0].permute(2, 0, 1).reshape(1, B, H, H).contiguous()
+
+    def make(n_total, n_burn):
+        return MHsampler.from_tiles(tiles, prior, model, 0.1, 2.5, p["flux_detection_threshold"],
+                                    n_total, n_burn, keep, print_every=10 ** 9,
+                                    seed=12345 + rank, device=dev)
+    make(1001, 1).run()  # warm-up
+    s = make(total, burnin)
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s.run()
+    torch.cuda.synchronize()
+    if world > 1:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t)
+    iters = B * (total - 1)
+    return {
+        "metric": "chain-iterations/sec (mcmc workload: MHsampler, 8x8 M71 cutouts)",
+        "value": world * iters / elapsed, "unit": "chain-iterations/sec", "n_gpus": world,
+        "steps": 1, "warmup": 1, "ms_per_step": elapsed * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (M71 truth prior at the real source density, seed 2000+rank)",
+        "config": {"workload": f"MCMC: {B} x 8x8 M71 cutouts/GPU, one chain each, S={S}, "
+                               f"{total} samples, burn-in {burnin}, every {keep}th kept",
+                   "tiles_per_gpu": B, "sources": S, "samples": total,
+                   "parallelism": f"image-sharded x{world}"},
+        "per_image_runtime_s": elapsed / B,
+        "acc_rate": float(s.accept.float().mean()),
+    }
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -237,6 +299,13 @@ def main():
 
     if args.workload != "c2" and args.tiles_per_gpu == 1:
         args.tiles_per_gpu = 42  # 332 M71 cutouts over 8 GPUs (manuscript.tex:562)
+    if args.workload == "mcmc":
+        out = bench_mcmc(args, dev, rank, world)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if dist:
+            tdist.destroy_process_group()
+        return
     s, mh, steps_per_step, cpu_tile, cfg = build_sampler(args, dev, rank)
     s.initialize()
     s._temper_reweight(with_resample=True)
