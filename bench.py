@@ -47,7 +47,7 @@ HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md (spec)
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md (vector FP32, spec)
 B_ALG_PER_STEP = 248        # SURVEY §8d, S=10
 F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
-PMC_FILE = "pmc_mh_r01_s2.json"  # rocprofv3 FETCH_SIZE+WRITE_SIZE per MH launch (scripts/profile.sh)
+PMC_FILE = "pmc_mh_r01_s3.json"  # rocprofv3 FETCH_SIZE+WRITE_SIZE per MH launch (scripts/profile.sh)
 
 
 def parse():
@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--kernel", choices=["mh", "mala"], default="mh")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # skip the untimed complete run() (wall time to temperature 1), e.g. under
+    # a profiler whose kernel averages should cover the timed steps only
+    ap.add_argument("--no-full-run", action="store_true")
     return ap.parse_args()
 
 
@@ -284,6 +287,21 @@ def bench_mcmc(args, dev, rank, world):
     }
 
 
+def _full_run(s2):
+    """One complete run() on a fresh sampler: initialise, the SMC loop with its
+    per-iteration stopping check, final resample, prune."""
+    import contextlib
+    import io
+    s2.print_every = 10 ** 9
+    s2.max_smc_iters = 500
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with contextlib.redirect_stdout(io.StringIO()):
+        s2.run()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -394,20 +412,15 @@ def main():
     # SURVEY §8d also asks for the wall time to temperature 1: one complete
     # run() (initialise, SMC loop with its per-iteration stopping check, final
     # resample, prune) on a fresh sampler, outside the timed region
-    s2, _, _, _, _ = build_sampler(args, dev, rank)
-    s2.print_every = 10 ** 9
-    s2.max_smc_iters = 500
-    import contextlib
-    import io
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    with contextlib.redirect_stdout(io.StringIO()):
-        s2.run()
-    torch.cuda.synchronize()
-    run_s = time.perf_counter() - t0
-    out["smc"]["run_to_tau1"] = {"iterations": int(s2.iter), "wall_s": run_s,
-                                 "ms_per_iteration": run_s / max(int(s2.iter), 1) * 1e3,
-                                 "temperature_min": float(s2.temperature.min())}
+    if args.no_full_run:
+        s2 = None
+    else:
+        s2, _, _, _, _ = build_sampler(args, dev, rank)
+    if s2 is not None:
+        run_s = _full_run(s2)
+        out["smc"]["run_to_tau1"] = {"iterations": int(s2.iter), "wall_s": run_s,
+                                     "ms_per_iteration": run_s / max(int(s2.iter), 1) * 1e3,
+                                     "temperature_min": float(s2.temperature.min())}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
         try:
             out["cpu_baseline"] = cpu_baseline(args, cpu_tile.cpu().numpy(),
