@@ -21,13 +21,14 @@
 #ifndef SMCDET_HIP_H
 #define SMCDET_HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 8
+#define SMCDET_ABI_VERSION 9
 
 /* status codes */
 #define SMCDET_OK 0
@@ -122,6 +123,13 @@ const char* smcdet_version(void);
 int32_t smcdet_abi_version(void);
 const char* smcdet_last_error(void);
 
+/* Pinned, device-mapped host memory (hipHostMalloc): *host is the host
+ * address, *device the address kernels use; zero-filled.  For small
+ * device->host signals without a copy launch (smcdet_temper_reweight's
+ * live_host).  Free with smcdet_host_free(host). */
+int smcdet_host_alloc(size_t bytes, void** host, void** device);
+int smcdet_host_free(void* host);
+
 /* ImageModel.loglikelihood / M71ImageModel.loglikelihood
  * (smcdet/images.py:85-102, :159-175): out[T,N]. */
 int smcdet_loglik(const smcdet_image_model_t* model, const float* tiled_image,
@@ -174,7 +182,10 @@ int smcdet_prior_sample(const smcdet_prior_t* prior, int32_t T,
  * image of particle ancestors[t,n] instead of re-rendering all S sources;
  * rate_out receives the image of the returned state (maintained
  * incrementally, float32 update rounding).  rate_in must describe *_in
- * exactly; rate_in != rate_out when ancestors is non-null. */
+ * exactly; rate_in != rate_out when ancestors is non-null.
+ * go (nullable, int32 device scalar): when *go == 0 the launch does nothing
+ * (no output is written) -- lets a host enqueue the next SMC iteration before
+ * it has read the loop condition (see smcdet_temper_reweight's `live`). */
 int smcdet_mh_sweep(const smcdet_image_model_t* model,
                     const smcdet_prior_t* prior, const smcdet_mh_t* mh,
                     const float* tiled_image, const float* temperature,
@@ -185,7 +196,7 @@ int smcdet_mh_sweep(const smcdet_image_model_t* model,
                     float* rate_out, uint64_t seed,
                     uint64_t offset, const smcdet_mh_replay_t* replay,
                     uint32_t flags, float* loglik_out, float* acc_rate,
-                    int32_t* acc_count, void* stream);
+                    int32_t* acc_count, const int32_t* go, void* stream);
 
 /* SingleComponentMALA.run (smcdet/kernel.py:133-275), K iterations fused in
  * one launch.  Arguments as smcdet_mh_sweep; mala->locs_stdev and
@@ -194,7 +205,7 @@ int smcdet_mh_sweep(const smcdet_image_model_t* model,
  * (h, w, f) -- what torch.autograd.grad computes (kernel.py:160-166,
  * :190-197) -- is evaluated analytically in-kernel over the source's PSF
  * window.  Flags: SMCDET_MH_COMPONENT_BY_COUNT, SMCDET_MH_SKIP_DONE.
- * The replay layout is smcdet_mh_replay_t's. */
+ * The replay layout is smcdet_mh_replay_t's; `go` as smcdet_mh_sweep. */
 int smcdet_mala_sweep(const smcdet_image_model_t* model,
                       const smcdet_prior_t* prior, const smcdet_mh_t* mala,
                       const float* tiled_image, const float* temperature,
@@ -205,7 +216,7 @@ int smcdet_mala_sweep(const smcdet_image_model_t* model,
                       float* rate_out, uint64_t seed,
                       uint64_t offset, const smcdet_mh_replay_t* replay,
                       uint32_t flags, float* loglik_out, float* acc_rate,
-                      int32_t* acc_count, void* stream);
+                      int32_t* acc_count, const int32_t* go, void* stream);
 
 /* MHsampler.run (smcdet/sampler.py:301-486): one single-component MH chain
  * per (tile, chain) at temperature 1 -- C chains per tile, T tiles (the
@@ -262,7 +273,10 @@ int smcdet_resample_index(const float* weights, int32_t T, int32_t N,
  * iteration).  live [3] (nullable, int32, zero before the first call): after
  * the call live[2] = the number of tiles still below temperature 1 (the
  * reference's while condition, sampler.py:230); live[0..1] are workspace and
- * left zero. */
+ * left zero.  go (nullable): when *go == 0 the launch does nothing.
+ * live_host (nullable, used with live): pinned, device-accessible host memory
+ * (hipHostMalloc) that also receives live[2], so a host can read the count
+ * once the launch has completed without enqueueing a copy. */
 int smcdet_temper_reweight(const float* loglik, float* temperature,
                            float* temperature_prev, float* log_weights_unnorm,
                            float* weights, float* ess, float* log_norm_const,
@@ -270,7 +284,7 @@ int smcdet_temper_reweight(const float* loglik, float* temperature,
                            int32_t resample_method, uint64_t seed,
                            uint64_t offset, int64_t* idx, uint32_t flags,
                            int32_t* finished_iter, int32_t iter, int32_t* live,
-                           void* stream);
+                           const int32_t* go, int32_t* live_host, void* stream);
 
 /* Gather of the resampled state (smcdet/sampler.py:150-169). */
 int smcdet_gather(const int64_t* idx, int32_t T, int32_t N, int32_t S,

@@ -92,7 +92,7 @@ def main():
         "tile_kernel": lambda: _hip.check(_hip.lib().smcdet_temper_reweight(
             _hip.ptr(ll), _hip.ptr(torch.zeros(T, device=dev)), _hip.ptr(tp), _hip.ptr(lw),
             _hip.ptr(W), _hip.ptr(ess), _hip.ptr(lz), T, Np, 0.5 * Np, 1, 1, 0, _hip.ptr(idx),
-            0, None, 0, None, _hip.stream_of(ll)), "tr"),
+            0, None, 0, None, None, None, _hip.stream_of(ll)), "tr"),
         "temper_only": lambda: _hip.check(_hip.lib().smcdet_temper(
             _hip.ptr(ll), _hip.ptr(torch.zeros(T, device=dev)), _hip.ptr(tp), T, Np, 0.5 * Np,
             _hip.stream_of(ll)), "t"),

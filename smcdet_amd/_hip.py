@@ -59,6 +59,8 @@ class ReplayC(ctypes.Structure):
 _SIGS = {
     "smcdet_version": ([], ctypes.c_char_p),
     "smcdet_abi_version": ([], c_i),
+    "smcdet_host_alloc": ([ctypes.c_size_t, c_p, c_p], c_i),
+    "smcdet_host_free": ([c_p], c_i),
     "smcdet_last_error": ([], ctypes.c_char_p),
     "smcdet_loglik": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
     "smcdet_render": ([c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
@@ -67,16 +69,17 @@ _SIGS = {
     "smcdet_log_prior": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
     "smcdet_prior_sample": ([c_p, c_i, c_i, c_u64, c_u64, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
     "smcdet_mh_sweep": ([c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p,
-                         c_p, c_p, c_p, c_u64, c_u64, c_p, c_u32, c_p, c_p, c_p, c_p], c_i),
+                         c_p, c_p, c_p, c_u64, c_u64, c_p, c_u32, c_p, c_p, c_p, c_p, c_p], c_i),
     "smcdet_mala_sweep": ([c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p,
-                           c_p, c_p, c_p, c_u64, c_u64, c_p, c_u32, c_p, c_p, c_p, c_p], c_i),
+                           c_p, c_p, c_p, c_u64, c_u64, c_p, c_u32, c_p, c_p, c_p, c_p, c_p],
+                          c_i),
     "smcdet_mh_chain": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_i, c_i, c_i, c_i,
                          c_i, c_u64, c_u64, c_p, c_p, c_p, c_p, c_p], c_i),
     "smcdet_temper": ([c_p, c_p, c_p, c_i, c_i, c_d, c_p], c_i),
     "smcdet_update_weights": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p], c_i),
     "smcdet_resample_index": ([c_p, c_i, c_i, c_i, c_u64, c_u64, c_p, c_p, c_p], c_i),
     "smcdet_temper_reweight": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_d, c_i, c_u64,
-                                c_u64, c_p, c_u32, c_p, c_i, c_p, c_p], c_i),
+                                c_u64, c_p, c_u32, c_p, c_i, c_p, c_p, c_p, c_p], c_i),
     "smcdet_gather": ([c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
     "smcdet_count_posterior": ([c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_u64, c_u64, c_p, c_p,
                                 c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
@@ -136,3 +139,30 @@ def dev_f32(t, name):
 
 def ref(x):
     return ctypes.byref(x)
+
+
+class HostInts:
+    """n int32 in pinned, device-mapped host memory (smcdet_host_alloc):
+    `dev(i)` is the device address of element i, `[i]` reads it on the host."""
+
+    def __init__(self, n):
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib().smcdet_host_alloc(4 * n, ctypes.byref(h), ctypes.byref(d)),
+              "smcdet_host_alloc")
+        self._h, self._d, self.n = h, d, n
+        self._view = (ctypes.c_int32 * n).from_address(h.value)
+
+    def dev(self, i):
+        return ctypes.c_void_p(self._d.value + 4 * i)
+
+    def __getitem__(self, i):
+        return int(self._view[i])
+
+    def __setitem__(self, i, v):
+        self._view[i] = int(v)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.smcdet_host_free(h)
+            self._h = None

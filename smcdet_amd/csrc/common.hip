@@ -1,4 +1,5 @@
 // common.hip — error state, version, model pre-digestion for the C ABI.
+#include <string.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -122,5 +123,27 @@ extern "C" {
 const char* smcdet_version(void) { return "smcdet_hip 0.1.0 (gfx950)"; }
 int32_t smcdet_abi_version(void) { return SMCDET_ABI_VERSION; }
 const char* smcdet_last_error(void) { return smcdet::g_err; }
+
+int smcdet_host_alloc(size_t bytes, void** host, void** device) {
+  using namespace smcdet;
+  if (!host || !device || bytes == 0) return set_error(SMCDET_EINVAL, "bad host_alloc args");
+  *host = nullptr;
+  *device = nullptr;
+  if (hipHostMalloc(host, bytes, hipHostMallocMapped) != hipSuccess)
+    return set_error(SMCDET_EHIP, "hipHostMalloc(%zu) failed", bytes);
+  if (hipHostGetDevicePointer(device, *host, 0) != hipSuccess) {
+    (void)hipHostFree(*host);
+    *host = nullptr;
+    return set_error(SMCDET_EHIP, "hipHostGetDevicePointer failed");
+  }
+  memset(*host, 0, bytes);
+  return SMCDET_OK;
+}
+
+int smcdet_host_free(void* host) {
+  if (host && hipHostFree(host) != hipSuccess)
+    return smcdet::set_error(SMCDET_EHIP, "hipHostFree failed");
+  return SMCDET_OK;
+}
 
 }  // extern "C"

@@ -61,6 +61,7 @@ struct MalaArgs {
   float* loglik_out;
   const float* rate_in;
   float* rate_out;
+  const int32_t* go;                 // predicate: skip the launch when *go == 0 (or null)
   int32_t* acc_count;
   float* acc_rate;
   const int32_t* r_comp;
@@ -73,6 +74,7 @@ template <int MODEL, bool REPLAY>
 __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
   extern __shared__ float smem[];
   __shared__ int wg_acc, wg_done;
+  if (a.go && *a.go == 0) return;
   const DevModel& m = a.m;
   const int HW = m.H * m.W;
   const int HWp = HW + kWave;
@@ -366,7 +368,7 @@ extern "C" int smcdet_mala_sweep(const smcdet_image_model_t* model, const smcdet
                                  float* rate_out, uint64_t seed, uint64_t offset,
                                  const smcdet_mh_replay_t* replay, uint32_t flags,
                                  float* loglik_out, float* acc_rate, int32_t* acc_count,
-                                 void* stream) {
+                                 const int32_t* go, void* stream) {
   int rc = validate_model(model);
   if (rc) return rc;
   rc = validate_prior(prior);
@@ -429,6 +431,7 @@ extern "C" int smcdet_mala_sweep(const smcdet_image_model_t* model, const smcdet
   a.rate_out = rate_out;
   a.acc_count = acc_count;
   a.acc_rate = acc_rate;
+  a.go = go;
   if (replay) {
     a.r_comp = replay->comp;
     a.r_uloc = replay->uloc;

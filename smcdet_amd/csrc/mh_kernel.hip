@@ -72,6 +72,7 @@ struct MhArgs {
   float* loglik_out;                 // [T,N] or null
   const float* rate_in;              // [T,N,H*W] persisted rate images or null
   float* rate_out;                   // [T,N,H*W] or null
+  const int32_t* go;                 // predicate: skip the launch when *go == 0 (or null)
   int32_t* acc_count;                // [2T] zeroed workspace: counts, tickets
   float* acc_rate;                   // [T]
   const int32_t* r_comp;             // replay (or null)
@@ -196,6 +197,7 @@ template <int MODEL, bool REPLAY, bool FULL, int PPL, bool PAIRED>
 __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   extern __shared__ float smem[];
   __shared__ int wg_acc, wg_done;  // last-iteration accepts / finished waves of this workgroup
+  if (a.go && *a.go == 0) return;  // speculatively enqueued sweep that must not run
   const DevModel& m = a.m;
   [[maybe_unused]] const int trow = (int)(blockIdx.x * kMhWaves + (threadIdx.x >> 6));
   SMC_TRACE(trow, 0);
@@ -756,7 +758,7 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
                                float* rate_out, uint64_t seed,
                                uint64_t offset, const smcdet_mh_replay_t* replay, uint32_t flags,
                                float* loglik_out, float* acc_rate, int32_t* acc_count,
-                               void* stream) {
+                               const int32_t* go, void* stream) {
   int rc = validate_model(model);
   if (rc) return rc;
   rc = validate_prior(prior);
@@ -812,6 +814,7 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
   a.rate_out = rate_out;
   a.acc_count = acc_count;
   a.acc_rate = acc_rate;
+  a.go = go;
   if (replay) {
     a.r_comp = replay->comp;
     a.r_uloc = replay->uloc;

@@ -46,6 +46,8 @@ struct TileArgs {
   int32_t* fin_iter;         // [T] SMC iteration a tile reached temperature 1 (-1: not yet) or null
   int32_t iter;              // the caller's SMC iteration number
   int32_t* live;             // [3] zeroed workspace: counter, ticket, tiles still below 1 (or null)
+  const int32_t* go;         // predicate: skip the launch when *go == 0 (or null)
+  int32_t* live_host;        // host-mapped copy of live[2] (pinned host memory) or null
 };
 
 // end-of-temper bookkeeping, thread 0 of each tile: the iteration at which the
@@ -58,8 +60,13 @@ __device__ __forceinline__ void tile_status(const TileArgs& a, int t, float tnew
     atomicAdd(&a.live[0], tnew < 1.0f ? 1 : 0);
     __threadfence();
     if (atomicAdd(&a.live[1], 1) == a.T - 1) {
-      a.live[2] = atomicExch(&a.live[0], 0);
+      const int nlive = atomicExch(&a.live[0], 0);
+      a.live[2] = nlive;
       atomicExch(&a.live[1], 0);
+      if (a.live_host) {  // the host reads it after the launch completes: no copy launch
+        *reinterpret_cast<volatile int32_t*>(a.live_host) = nlive;
+        __threadfence_system();
+      }
     }
   }
 }
@@ -251,6 +258,7 @@ __device__ double block_brentq(F&& f, double xa, double xb, double fa, double fb
 
 template <int PER>
 __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
+  if (a.go && *a.go == 0) return;  // speculatively enqueued iteration that must not run
   extern __shared__ float buf[];  // N floats: weights / cumsum, then N+1 resample slots
   __shared__ TileRed red;
   int parity = 0;
@@ -756,7 +764,7 @@ int smcdet_temper_reweight(const float* loglik, float* temperature, float* tempe
                            float* log_norm_const, int32_t T, int32_t N, double ess_threshold,
                            int32_t resample_method, uint64_t seed, uint64_t offset, int64_t* idx,
                            uint32_t flags, int32_t* finished_iter, int32_t iter, int32_t* live,
-                           void* stream) {
+                           const int32_t* go, int32_t* live_host, void* stream) {
   if (!loglik || !temperature || !temperature_prev || !log_weights_unnorm || !weights || !ess ||
       !log_norm_const)
     return set_error(SMCDET_EINVAL, "null buffer");
@@ -785,6 +793,8 @@ int smcdet_temper_reweight(const float* loglik, float* temperature, float* tempe
   a.fin_iter = finished_iter;
   a.iter = iter;
   a.live = live;
+  a.go = go;
+  a.live_host = live ? live_host : nullptr;
   return launch_tile(a, (hipStream_t)stream);
 }
 

@@ -96,13 +96,15 @@ class SingleComponentMH(object):
 
     def run(self, data, counts, locs, fluxes, temperature, log_target=None, *, prior=None,
             image_model=None, ancestors=None, replay=None, want_loglik=True, rate_in=None,
-            rate_out=None, flags=0):
+            rate_out=None, flags=0, go=None):
         """kernel.py:26-130.  ancestors [numH,numW,N] (int64, optional) gathers
         the starting state (a fused resample); replay = dict(comp, uloc, uflux,
         uacc) replays recorded draws; rate_in / rate_out [numH,numW,N,H*W]
         (optional) are persisted per-particle rate images: rate_in must be the
         images of (locs, fluxes), rate_out receives those of the result
-        (ignored in full_recompute mode)."""
+        (ignored in full_recompute mode).  go (int32 device scalar, optional):
+        the launch does nothing when *go == 0 (speculative enqueue, see
+        SMCsampler.run)."""
         prior, image_model = self._resolve(log_target, prior, image_model)
         data = _hip.dev_f32(data, "data")
         counts = _hip.dev_f32(counts, "counts")
@@ -155,7 +157,7 @@ class SingleComponentMH(object):
             _hip.ptr(self._rate_buffer(rate_out, "rate_out", T * N, data)),
             self.rng.seed, off,
             _hip.ref(rp) if rp is not None else None, flags, _hip.ptr(ll), _hip.ptr(acc),
-            _hip.ptr(acc_ws), _hip.stream_of(locs)), self._entry)
+            _hip.ptr(acc_ws), _hip.ptr(go), _hip.stream_of(locs)), self._entry)
         if ev is not None:
             e1.record(torch.cuda.current_stream(dev))
             ev.append((e0, e1))

@@ -243,6 +243,8 @@ class SMCsampler(object):
         kw = {} if rout is None else {"rate_in": rin, "rate_out": rout}
         if self.stopping == "independent":
             kw["flags"] = _hip.SMCDET_MH_SKIP_DONE
+        if getattr(self, "_go", None) is not None:
+            kw["go"] = self._go
         self.locs, self.fluxes, self.mutation_acc_rates = self.MutationKernel.run(
             self.tiled_image, self.counts, self.locs, self.fluxes, self.temperature,
             self.log_target, ancestors=ancestors, **kw)
@@ -270,6 +272,7 @@ class SMCsampler(object):
         self.weights_log_unnorm = torch.empty_like(self.loglik)
         self.weights = torch.empty_like(self.loglik)
         self.ess = torch.empty_like(new_t)
+        live = self._live_ws()
         idx = None
         off = 0
         if with_resample:
@@ -281,20 +284,28 @@ class SMCsampler(object):
             _hip.ptr(self.log_normalizing_constant), self._T, N, float(self.ess_threshold),
             self._method_code(), self.rng.seed, off, _hip.ptr(idx),
             _hip.SMCDET_SMC_FREEZE_DONE if self.stopping == "independent" else 0,
-            _hip.ptr(self.iters_per_tile), int(getattr(self, "iter", 0)), _hip.ptr(self._live_ws()),
+            _hip.ptr(self.iters_per_tile), int(getattr(self, "iter", 0)), _hip.ptr(live),
+            _hip.ptr(getattr(self, "_go", None)), getattr(self, "_live_host", None),
             _hip.stream_of(new_t)), "smcdet_temper_reweight")
         self.temperature_prev = prev_t
         self.temperature = new_t
         self._pending_idx = idx
+        self._live = live
         self._live_valid = True
 
     def _live_ws(self):
-        """[3] int32 zeroed once; the tile kernel leaves the number of tiles
-        below temperature 1 in [2] (smcdet_temper_reweight)."""
-        ws = getattr(self, "_live", None)
-        if ws is None or ws.device != self.temperature.device:
-            ws = torch.zeros(3, device=self.temperature.device, dtype=torch.int32)
-            self._live = ws
+        """The next of two [3] int32 buffers (zeroed once, alternating per
+        call); the tile kernel leaves the number of tiles below temperature 1
+        in [2] (smcdet_temper_reweight).  Two, so that a speculatively
+        enqueued iteration can run while the previous count is read."""
+        bufs = getattr(self, "_live_bufs", None)
+        if bufs is None or bufs[0].device != self.temperature.device:
+            bufs = [torch.zeros(3, device=self.temperature.device, dtype=torch.int32)
+                    for _ in range(2)]
+            self._live_bufs = bufs
+            self._live_next = 0
+        ws = bufs[self._live_next]
+        self._live_next ^= 1
         return ws
 
     def _mark_finished(self):
@@ -328,6 +339,76 @@ class SMCsampler(object):
                         f"{round(acc.max().item(), 2)}]")
             print(msg)
 
+    # ------------------------------------------------------- speculative loop
+    _SNAPSHOT = ("locs", "fluxes", "counts", "mutation_acc_rates", "_fresh_loglik", "loglik",
+                 "weights", "weights_log_unnorm", "ess", "temperature_prev", "_pending_idx",
+                 "_rate_cur", "_rate_age", "_rate_valid", "_live", "_live_next", "iter")
+    _host_flags = None
+
+    def _can_speculate(self):
+        """The speculative loop needs the default stopping rule and schedule
+        hooks (the distributed lockstep mode and instrumented test samplers
+        replace them) and a kernel that honours the `go` predicate."""
+        return ("_keep_going" not in self.__dict__ and "_temper_reweight" not in self.__dict__
+                and "mutate" not in self.__dict__
+                and hasattr(self.MutationKernel, "_entry"))
+
+    def _run_speculative(self):
+        """sampler.py:230-237 without a host round trip per iteration: the
+        next iteration is enqueued BEFORE the previous loop condition is known,
+        predicated on the device-side count of unfinished tiles (`go`: the
+        kernels return immediately when it is 0).  The tile kernel also writes
+        the count into pinned, device-mapped host memory, which the host reads
+        once that launch's event has completed -- while the GPU already works
+        on the next iteration (no copy launch, which would queue behind the
+        full-occupancy MH sweep).  When the count turns out to be 0, the enqueued
+        iteration did nothing on the device and its host-side bookkeeping
+        (attribute rebinding, random-stream offsets) is rolled back, so the
+        result is identical to the synchronous loop."""
+        main = torch.cuda.current_stream(self.device)
+        # the tile kernel writes each iteration's count of unfinished tiles into
+        # pinned, device-mapped host memory (two slots, alternating) next to
+        # its device copy
+        if getattr(self, "_host_flags", None) is None:
+            self._host_flags = _hip.HostInts(2)
+        pinned = self._host_flags
+
+        def launched():
+            ev = torch.cuda.Event()
+            ev.record(main)
+            return ev
+
+        # the initial temper/reweight has run synchronously with respect to the
+        # host count: read it from the device copy once
+        pinned[0] = int(self._live[2])
+        live_prev, slot = self._live, 0
+        ev_prev = None
+        try:
+            while self.iter <= self.max_smc_iters:
+                snap = {k: getattr(self, k, None) for k in self._SNAPSHOT}
+                rng_off = self.rng.offset
+                self.iter += 1
+                self._print_progress()
+                self._go = live_prev[2:3]
+                self._live_host = pinned.dev(1 - slot)
+                idx, self._pending_idx = self._pending_idx, None
+                self.mutate(ancestors=idx)
+                self._temper_reweight(with_resample=True)
+                self._go = self._live_host = None
+                ev = launched()
+                if ev_prev is not None:
+                    ev_prev.synchronize()
+                if int(pinned[slot]) == 0:
+                    # every tile had finished: the iteration just enqueued was a no-op
+                    for k, v in snap.items():
+                        setattr(self, k, v)
+                    self.rng.offset = rng_off
+                    break
+                live_prev, ev_prev, slot = self._live, ev, 1 - slot
+        finally:
+            self._go = self._live_host = None
+            torch.cuda.synchronize(self.device)
+
     def _keep_going(self):
         """sampler.py:230: continue while any tile has temperature < 1 (one
         device->host read per SMC iteration; after the fused temper launch the
@@ -341,7 +422,10 @@ class SMCsampler(object):
         self.iter = 0
         print("starting...")
         self.initialize()
-        if self.fused:
+        if self.fused and self._can_speculate():
+            self._temper_reweight(with_resample=True)
+            self._run_speculative()
+        elif self.fused:
             self._temper_reweight(with_resample=True)
             while self._keep_going() and self.iter <= self.max_smc_iters:
                 self.iter += 1

@@ -29,7 +29,7 @@ def test_every_header_symbol_is_exported_and_bound():
 
 
 def test_version_and_abi():
-    assert _hip.lib().smcdet_abi_version() == 8
+    assert _hip.lib().smcdet_abi_version() == 9
     assert "gfx950" in _hip.version()
 
 

@@ -81,3 +81,29 @@ def test_batch_logz_matches_reference_stats():
     se = np.sqrt(lz.var(ddof=1) / len(lz) + lz_ref.var(ddof=1) / len(lz_ref))
     assert abs(lz.mean() - lz_ref.mean()) <= 3 * se, (lz.mean(), lz_ref.mean(), se)
     assert abs(lz.mean() - lz_ref.mean()) <= 0.01 * abs(lz_ref.mean())
+
+
+def test_speculative_loop_equals_synchronous_loop():
+    """SMCsampler.run() enqueues each SMC iteration before reading the
+    previous loop condition (kernels predicated on the device-side count of
+    unfinished tiles) and rolls back the one no-op iteration at the end: the
+    result must equal the synchronous loop's exactly."""
+    from smcdet_amd.sampler import SMCsampler
+    images = _images(4, 8, 7)
+    outs = []
+    for speculative in (True, False):
+        s = SMCsampler.from_tiles(images.reshape(1, 4, 8, 8), p_m71_prior(8, 4, 4),
+                                  p_m71_model(8), p_m71_mh(20), 256, 0.5, "systematic",
+                                  M71["flux_detection_threshold"], 100, print_every=10 ** 9,
+                                  seed=13, device=DEV)
+        if not speculative:
+            s._keep_going = s._keep_going  # an instance hook selects the synchronous loop
+        assert s._can_speculate() == speculative
+        s.run()
+        outs.append(s)
+    a, b = outs
+    assert a.iter == b.iter
+    for k in ("locs", "fluxes", "counts", "log_normalizing_constant", "temperature", "ess",
+              "weights", "pruned_counts", "iters_per_tile"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    assert a.rng.offset == b.rng.offset
