@@ -349,8 +349,9 @@ class SMCsampler(object):
         """The speculative loop needs the default stopping rule and schedule
         hooks (the distributed lockstep mode and instrumented test samplers
         replace them) and a kernel that honours the `go` predicate."""
-        return ("_keep_going" not in self.__dict__ and "_temper_reweight" not in self.__dict__
-                and "mutate" not in self.__dict__
+        hooks = ("_keep_going", "_temper_reweight", "mutate")
+        return (all(h not in self.__dict__ and getattr(type(self), h) is getattr(SMCsampler, h)
+                    for h in hooks)
                 and hasattr(self.MutationKernel, "_entry"))
 
     def _run_speculative(self):
