@@ -22,7 +22,8 @@
 //   * one pass over the new window (delta log-likelihood, the rate after the
 //     move, the gradient at the proposal) and one over the old window's
 //     remaining positions (delta log-likelihood); the moved rates go to an
-//     LDS scratch and are written back on accept;
+//     LDS scratch and are written back on accept; the source's PSF at its
+//     current place comes from an LDS cache filled by the gradient pass;
 //   * accept iff U <= min(1, exp(log alpha)); log alpha in the finite regime
 //     is the exact difference (delta log target + Hastings terms, no float32
 //     absorption of a ~1e3-1e4 log target), proposals on the location box's
@@ -83,8 +84,9 @@ __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
   constexpr int kImg = (MODEL == SMCDET_MODEL_POISSON) ? 2 : 1;
   float* xs = smem;
   float* lg = smem + HWp;
-  float* lam = smem + kImg * HWp + wave * (HWp + 2 * a.W2);
+  float* lam = smem + kImg * HWp + wave * (HWp + 3 * a.W2);
   float* scr = lam + HWp;  // moved rates: new window [0, W2), old-only [W2, 2 W2)
+  float* psc = scr + 2 * a.W2;  // raw psf of the moved source at its current place, per old-window position
 
   stage_image<MODEL>(a.img + (size_t)t * HW, xs, lg, HW, threadIdx.x, kMalaBlock);
   if (threadIdx.x == 0) {
@@ -164,6 +166,7 @@ __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
       const float dh = ((float)ph + 0.5f) - h, dw = ((float)pw + 0.5f) - w;
       float dpsi;
       const float psi = psf_raw_d<MODEL>(m, fmaf(dh, dh, dw * dw), dpsi);
+      psc[i] = psi;  // reused by the delta passes (the same value bit for bit)
       const int p = ph * m.W + pw;
       const float e = dll_drate<MODEL>(m, xs[p], lam[p]);
       gf = fmaf(e, psi, gf);
@@ -174,6 +177,7 @@ __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
     gr[0] = wave_sum(gh);
     gr[1] = wave_sum(gw);
     gr[2] = wave_sum(gf);
+    wave_sync();  // psc[] written by all lanes before the delta passes read it
   };
 
   int accept = 0;
@@ -221,10 +225,7 @@ __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
       float dpsi;
       const float psi_n = psf_raw_d<MODEL>(m, fmaf(dhn, dhn, dwn * dwn), dpsi);
       float psi_o = 0.f;
-      if (in_window(m, qo.fh, qo.fw, ph, pw)) {
-        const float dho = fph - h, dwo = fpw - w;
-        psi_o = psf_raw<MODEL>(m, fmaf(dho, dho, dwo * dwo));
-      }
+      if (in_window(m, qo.fh, qo.fw, ph, pw)) psi_o = psc[(ph - qo.r0) * qo.bw + (pw - qo.c0)];
       const float dl = fmaf(amp_n, psi_n, -amp_o * psi_o);
       const int p = ph * m.W + pw;
       const float lo = lam[p], x = xs[p];
@@ -243,8 +244,7 @@ __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
       int ph, pw;
       window_pos(qo, i, ph, pw);
       if (in_window(m, qn.fh, qn.fw, ph, pw)) continue;
-      const float dho = ((float)ph + 0.5f) - h, dwo = ((float)pw + 0.5f) - w;
-      const float dl = -amp_o * psf_raw<MODEL>(m, fmaf(dho, dho, dwo * dwo));
+      const float dl = -amp_o * psc[i];
       const int p = ph * m.W + pw;
       const float lo = lam[p];
       const float lgx = (MODEL == SMCDET_MODEL_POISSON) ? lg[p] : 0.0f;
@@ -440,7 +440,7 @@ extern "C" int smcdet_mala_sweep(const smcdet_image_model_t* model, const smcdet
   }
   const size_t HWp = (size_t)model->H * model->W + kWave;
   const size_t lds = ((model->model == SMCDET_MODEL_POISSON ? 2 : 1) * HWp +
-                      (size_t)kMalaWaves * (HWp + 2 * (size_t)a.W2)) *
+                      (size_t)kMalaWaves * (HWp + 3 * (size_t)a.W2)) *
                      sizeof(float);
   const dim3 grid((N + kMalaWaves - 1) / kMalaWaves, T);
   hipStream_t st = (hipStream_t)stream;
