@@ -203,3 +203,35 @@ def test_mala_batch_independent_vs_lockstep():
     np.testing.assert_array_equal(N(res[0]["num_iters"]), N(res[1]["num_iters"]))
     np.testing.assert_array_equal(N(res[0]["log_normalizing_constant"]),
                                   N(res[1]["log_normalizing_constant"]))
+
+
+def test_mala_ragged_tiles_vs_oracle():
+    """Ragged N (37, not a multiple of the 4 particles per workgroup) over a
+    2x3 grid of tiles, replayed synthetic draws: kernel vs C restatement."""
+    from oracle.smc_oracle import MHParams
+    from smcdet_amd.kernel import SingleComponentMALA
+    H, S, Np, K = 8, 3, 37, 15
+    d = golden("mh_m71_tiles.npz")
+    img = np.ascontiguousarray(np.concatenate([tiles_of(d["image"], H)] * 2, 1)[:, :3])  # [2,3,8,8]
+    oprior = o_m71_prior(H, S, S)
+    rng = np.random.default_rng(11)
+    counts, locs, fluxes = O.prior_sample_stratified(
+        oprior, 1, Np, rng.random((1, 1, Np, S, 2)), rng.random((1, 1, Np, S)), np.float32)
+    rep = lambda a: np.ascontiguousarray(np.broadcast_to(a, (2, 3) + a.shape[2:]))  # noqa: E731
+    counts, locs, fluxes = (rep(x).astype(np.float32) for x in (counts, locs, fluxes))
+    rp = dict(comp=rng.integers(0, S, (K, 2, 3, Np)).astype(np.int32),
+              uloc=rng.random((K, 2, 3, Np, 2)).astype(np.float32),
+              uflux=rng.random((K, 2, 3, Np)).astype(np.float32),
+              uacc=rng.random((K, 2, 3, Np)).astype(np.float32))
+    tau = np.array([[0.2, 0.5, 1.0], [0.05, 0.7, 0.3]], np.float32)
+    ol, of_, oacc = c_oracle.mala_sweep(img, counts, locs, fluxes, tau, oprior, o_m71_model(H),
+                                        MHParams(K, 0.1, 2.5, M71["flux_lower"],
+                                                 M71["flux_upper"]), replay=rp, threads=8)
+    mala = SingleComponentMALA(K, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    l, f, acc = mala.run(T(img), T(counts), T(locs), T(fluxes), T(tau), prior=p_m71_prior(H, S, S),
+                         image_model=p_m71_model(H),
+                         replay={k: torch.as_tensor(v) for k, v in rp.items()})
+    close = (np.abs(N(l) - ol).max((-1, -2)) < 1e-3) & (np.abs(N(f) - of_).max(-1) <
+                                                         1e-3 * (1 + np.abs(of_).max(-1)))
+    assert close.mean() > 0.97, close.mean()
+    assert np.abs(N(acc) - oacc).max() <= 2.0 / Np + 1e-6

@@ -110,3 +110,45 @@ def test_mh_chain_many_chains_and_images():
     assert not np.allclose(per_chain[:, :, 0], per_chain[:, :, 1])
     assert 0.05 < float(s.accept.float().mean()) < 0.99
     assert s.posterior_mean_count(s.pruned_counts).shape == (1, 4)
+
+
+def test_mh_chain_poisson_many_chains_vs_oracle():
+    """Poisson ImageModel + ParetoStarPrior (the basic family) chains, C=5 per
+    tile (not a multiple of 4) on 2x2 tiles, replayed synthetic draws: every
+    chain against the C restatement."""
+    from oracle.smc_oracle import MHParams
+    from smcdet_amd.sampler import MHsampler
+    from tests._params import BASIC_FLUX_SCALE, o_basic_model, o_basic_prior, p_basic_model, \
+        p_basic_prior
+    H, S, C, total, burnin, keep = 8, 3, 5, 121, 20, 5
+    K = total - 1
+    d = golden("mh_basic_16x16.npz")
+    img = tiles_of(d["image"], H)                                        # [2,2,8,8]
+    rng = np.random.default_rng(3)
+    init_l = (rng.random((2, 2, C, S, 2)) * 10 - 1).astype(np.float32)
+    init_f = (BASIC_FLUX_SCALE * 0.9 * (1 + 3 * rng.random((2, 2, C, S)))).astype(np.float32)
+    rp = dict(comp=rng.integers(0, S, (K, 2, 2, C)).astype(np.int32),
+              uloc=rng.random((K, 2, 2, C, 2)).astype(np.float32),
+              uflux=rng.random((K, 2, 2, C)).astype(np.float32),
+              uacc=rng.random((K, 2, 2, C)).astype(np.float32))
+    prior = p_basic_prior(H, S, S)
+    prior.flux_lower, prior.flux_upper = BASIC_FLUX_SCALE * 0.9, 1e6
+    s = MHsampler(torch.as_tensor(d["image"], device=DEV), H, prior, p_basic_model(H), 0.1, 100,
+                  0.0, total, burnin, keep, print_every=10 ** 9, num_chains=C)
+    s.locs = torch.as_tensor(init_l, device=DEV)
+    s.fluxes = torch.as_tensor(init_f, device=DEV)
+    s.run(replay={k: torch.as_tensor(v) for k, v in rp.items()})
+    M = (total - burnin + keep - 1) // keep
+    gl = N(s.locs).reshape(2, 2, C, M, S, 2)
+    ga = N(s.accept)
+    ok = 0
+    for c in range(C):
+        sub = {k: np.ascontiguousarray(v[:, :, :, c]) for k, v in rp.items()}
+        ol, of_, oacc = c_oracle.mh_chain(img, np.full((2, 2), S, np.float32), init_l[:, :, c],
+                                          init_f[:, :, c], o_basic_prior(H, S, S), o_basic_model(H),
+                                          MHParams(1, 0.1, 100, BASIC_FLUX_SCALE * 0.9, 1e6),
+                                          total, burnin, keep, sub)
+        ok += (ga[:, :, c] == oacc).mean()
+        same = (ga[:, :, c] == oacc).all(-1)
+        np.testing.assert_allclose(gl[:, :, c][same], ol[same], rtol=0, atol=1e-3)
+    assert ok / C > 0.99
