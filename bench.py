@@ -68,6 +68,10 @@ def parse():
     ap.add_argument("--sources", type=int, default=10)
     ap.add_argument("--mh-iters", type=int, default=100)
     ap.add_argument("--tiles-per-gpu", type=int, default=1)
+    # c2 strong scaling (BASELINE configs[2], C3: 64 tiles over the GPUs): this
+    # many 32x32 tiles in total, split contiguously over the ranks; tile g is
+    # drawn from seed 1000 + g whatever the rank count
+    ap.add_argument("--total-tiles", type=int, default=0)
     ap.add_argument("--full-recompute", action="store_true")
     # mutation kernel: SingleComponentMH (the headline) or SingleComponentMALA
     # (smcdet/kernel.py:133-275) on the same workload, as an extra line
@@ -121,6 +125,26 @@ def synthetic_image(model, truth, H, tiles_per_side, seed, dev, max_sources):
     return img
 
 
+def synthetic_tiles(model, truth, H, tile_ids, dev, max_sources):
+    """[1, len(tile_ids), H, H] synthetic M71 tiles, tile g from seed 1000 + g."""
+    out = torch.empty(1, len(tile_ids), H, H, device=dev)
+    for i, g in enumerate(tile_ids):
+        torch.manual_seed(1000 + g)
+        while True:
+            c, l, f = truth.sample(num_catalogs=1, device=dev)
+            if int(c.max()) <= max_sources:
+                break
+        out[0, i] = model.sample(l, f)[0, 0, :, :, 0]
+    return out
+
+
+def shard(total, world, rank):
+    """Contiguous block of range(total) owned by `rank` (as distributed.shard_tiles)."""
+    base, rem = divmod(total, world)
+    lo = rank * base + min(rank, rem)
+    return list(range(lo, lo + base + (1 if rank < rem else 0)))
+
+
 def cpu_baseline(args, image_tile, seconds):
     """C restatement of the reference MH sweep (float64 full re-render per
     step, OpenMP over particles) on a bounded sample of the same workload."""
@@ -170,6 +194,24 @@ def build_sampler(args, dev, rank):
     """(sampler, particle-steps per SMC step, workload description)."""
     from smcdet_amd.sampler import SMCsampler
     p = M71
+    if args.workload == "c2" and args.total_tiles > 0:
+        H, S, Np, K = args.tile, args.sources, args.particles, args.mh_iters
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        ids = shard(args.total_tiles, world, rank)
+        if not ids:
+            raise SystemExit(f"rank {rank}: no tiles ({args.total_tiles} over {world} ranks)")
+        model, prior, truth = make_models(H, S)
+        tiles = synthetic_tiles(model, truth, H, ids, dev, S)
+        mh = mutation_kernel(args, K, args.full_recompute)
+        s = SMCsampler.from_tiles(tiles, prior, model, mh, Np, 0.5, "systematic",
+                                  p["flux_detection_threshold"], 10 ** 9, print_every=10 ** 9,
+                                  seed=12345 + rank, device=dev)
+        T = len(ids)
+        return s, mh, T * Np * K, tiles[0, 0], dict(
+            workload=f"C3: {args.total_tiles} x {H}x{H} tiles over {world} GPU(s) ({T} on rank "
+                     f"{rank}), S={S}, N={Np}, {K} {args.kernel.upper()} iters per SMC step, "
+                     "systematic, rho=0.5", total_tiles=args.total_tiles, tiles_per_gpu=T,
+            particles=Np, tile=H, sources=S, mh_iters=K, kernel=args.kernel)
     if args.workload == "c2":
         H, S, Np, K = args.tile, args.sources, args.particles, args.mh_iters
         tps = int(round(args.tiles_per_gpu ** 0.5))
@@ -358,7 +400,10 @@ def main():
         elapsed = float(t)
     mh_ms = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
 
-    value = world * steps_per_step * args.steps / elapsed
+    if args.total_tiles > 0:  # strong scaling: every rank's tiles, uneven shares included
+        value = args.total_tiles * args.particles * args.mh_iters * args.steps / elapsed
+    else:
+        value = world * steps_per_step * args.steps / elapsed
     launch_steps = steps_per_step  # particle-steps per MH launch
     # SURVEY §8d per-particle-step figures, for this workload's S and tile
     S_, HW_ = cfg["sources"], cfg["tile"] * cfg["tile"]
@@ -390,7 +435,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.total_tiles > 0 else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (M71 prior + image model, seed 1000+rank)",
