@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kChainBlock, 4) void mh_chain_kernel(ChainArgs a) {
   };
   if (a.k_begin == 0) record(0);
 
-  const int d = min(lane, 2);
+  const int d = lane % 3;  // proposal dimension of this lane (lanes 3.. replicate 0..2)
   const float dsig = d < 2 ? a.sl : a.sf, drs = d < 2 ? a.rsl : a.rsf;
   const float dlb = d == 0 ? a.lb_h : (d == 1 ? a.lb_w : a.lb_f);
   const float dub = d == 0 ? a.ub_h : (d == 1 ? a.ub_w : a.ub_f);
@@ -135,9 +135,10 @@ __global__ __launch_bounds__(kChainBlock, 4) void mh_chain_kernel(ChainArgs a) {
 
     // ---- proposal and Hastings terms (sampler.py:435-495) -------------------
     const float cur = d == 0 ? h : (d == 1 ? w : f);
-    const float xn = t_sample(cur, dsig, drs, dlb, dub, ud);
-    const float q_fwd = t_logprob(xn, cur, dsig, drs, dlb, dub);
-    const float q_rev = t_logprob(cur, xn, dsig, drs, dlb, dub);
+    const TnBox bc = t_box_lanes(cur, drs, dlb, dub, lane);
+    const float xn = t_sample_box(cur, dsig, dlb, dub, ud, bc);
+    const float q_fwd = t_logprob_box(xn, cur, dsig, bc);
+    const float q_rev = t_logprob_box(cur, xn, dsig, t_box_lanes(xn, drs, dlb, dub, lane));
     const float hn = readlane(xn, 0), wn = readlane(xn, 1), fn = readlane(xn, 2);
 
     // ---- delta log-likelihood over the new window and the old-only positions

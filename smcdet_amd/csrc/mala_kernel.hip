@@ -121,7 +121,7 @@ __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
   }
 
   // lane d < 3 owns proposal dimension d (h, w, flux)
-  const int d = min(lane, 2);
+  const int d = lane % 3;  // proposal dimension of this lane (lanes 3.. replicate 0..2)
   const float dsig = d < 2 ? a.sl : a.sf, drs = d < 2 ? a.rsl : a.rsf;
   const float dc = d < 2 ? a.cl : a.cf;
   const float dlb = d == 0 ? a.lb_h : (d == 1 ? a.lb_w : a.lb_f);
@@ -209,8 +209,9 @@ __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
 #pragma clang fp contract(off)
       mu = cur + dc * gd;
     }
-    const float xn = t_sample(mu, dsig, drs, dlb, dub, ud);
-    const float q_fwd = t_logprob(xn, mu, dsig, drs, dlb, dub);
+    const TnBox bf = t_box_lanes(mu, drs, dlb, dub, lane);
+    const float xn = t_sample_box(mu, dsig, dlb, dub, ud, bf);
+    const float q_fwd = t_logprob_box(xn, mu, dsig, bf);
     const float hn = readlane(xn, 0), wn = readlane(xn, 1), fn = readlane(xn, 2);
 
     // ---- new window: delta log-likelihood, moved rates, gradient at the proposal
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
 #pragma clang fp contract(off)
       mur = xn + dc * pgd;
     }
-    const float q_rev = t_logprob(cur, mur, dsig, drs, dlb, dub);
+    const float q_rev = t_logprob_box(cur, mur, dsig, t_box_lanes(mur, drs, dlb, dub, lane));
     const float f0 = readlane(q_fwd, 0), f1 = readlane(q_fwd, 1), f2 = readlane(q_fwd, 2);
     const float b0 = readlane(q_rev, 0), b1 = readlane(q_rev, 1), b2 = readlane(q_rev, 2);
 

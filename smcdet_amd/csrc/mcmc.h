@@ -73,6 +73,42 @@ __device__ __forceinline__ float t_logprob(float v, float mu, float sig, float r
   return lp - t_logZ(mu, rsig, lb, ub);
 }
 
+// The three proposal dimensions run in lanes d = lane % 3 (lanes 3..5 and up
+// replicate 0..2).  A dimension's two Normal.cdf evaluations (box bounds lb and
+// ub) run in two lanes at once -- lane d takes lb, lane d+3 takes ub -- and are
+// exchanged with a lane permute: one erf per wave instruction stream instead
+// of two, with the same values as t_logZ.
+struct TnBox {
+  float cdf_lb, logZ;  // Normal(mu, sigma).cdf(lb) and log_prob_in_box
+};
+__device__ __forceinline__ TnBox t_box_lanes(float mu, float rsig, float lb, float ub, int lane) {
+#pragma clang fp contract(off)
+  const float v = (lane >= 3 && lane < 6) ? ub : lb;
+  const float c = t_cdf(v, mu, rsig);
+  const int d = lane % 3;
+  TnBox b;
+  b.cdf_lb = __shfl(c, d, kWave);
+  b.logZ = nan_to_num(logf(__shfl(c, d + 3, kWave) - b.cdf_lb), 0.0f);
+  return b;
+}
+// t_sample / t_logprob with the box quantities of t_box_lanes
+__device__ __forceinline__ float t_sample_box(float mu, float sig, float lb, float ub, float u,
+                                              const TnBox& b) {
+#pragma clang fp contract(off)
+  const float lo = 1e-6f, hi = (float)(1.0 - 1e-6);
+  const float p = fminf(fmaxf(u, lo), hi);
+  float pt = b.cdf_lb + p * expf(b.logZ);
+  pt = fminf(fmaxf(pt, lo), hi);
+  const float x = mu + sig * erfinv_fast(2.0f * pt - 1.0f) * kSqrt2;
+  return fminf(fmaxf(x, lb), ub);
+}
+__device__ __forceinline__ float t_logprob_box(float v, float mu, float sig, const TnBox& b) {
+#pragma clang fp contract(off)
+  const float d = v - mu;
+  const float lp = -(d * d) / (2.0f * (sig * sig)) - logf(sig) - kHalfLog2Pi;
+  return lp - b.logZ;
+}
+
 // clipped (2R+1)^2 window anchored at floor(h, w)
 struct Window {
   int fh, fw;       // anchors
