@@ -17,7 +17,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from smcdet_amd import _hip  # noqa: E402
-from tests._params import M71, p_m71_mh, p_m71_model, p_m71_prior  # noqa: E402
+from tests._params import p_m71_mh, p_m71_model, p_m71_prior  # noqa: E402
 
 
 def main():

@@ -15,7 +15,7 @@ import torch
 
 from oracle import c_oracle
 from oracle import smc_oracle as O
-from tests._params import (M71, MALA_FIXTURES, golden, mala_fixture_setup, o_m71_model,
+from tests._params import (M71, MALA_FIXTURES, golden, o_m71_model,
                            o_m71_prior, p_m71_model, p_m71_prior, p_mala_fixture_setup,
                            tiles_of)
 

@@ -12,7 +12,7 @@ import pytest
 import torch
 
 from oracle import smc_oracle as O
-from tests._params import (M71, MH_FIXTURES, golden, mh_fixture_setup, o_m71_model,
+from tests._params import (M71, MH_FIXTURES, golden, o_m71_model,
                            p_basic_model, p_basic_prior, p_m71_model, p_m71_mh, p_m71_prior,
                            p_mh_fixture_setup, tiles_of)
 
