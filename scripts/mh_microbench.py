@@ -25,13 +25,15 @@ def main():
     ap.add_argument("--particles", type=int, default=4096)
     ap.add_argument("--tiles", type=int, default=1)
     ap.add_argument("--K", type=int, default=100)
+    ap.add_argument("--tile", type=int, default=32)
+    ap.add_argument("--sources", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--full", action="store_true", help="include the full-recompute variant")
     ap.add_argument("--only", default=None, help="run just this variant (for rocprofv3 --pmc)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    H, S, Np = 32, 10, a.particles
+    H, S, Np = a.tile, a.sources, a.particles
     nt = int(round(a.tiles ** 0.5))
     model, prior = p_m71_model(H), p_m71_prior(H, S, S, counts_rate=0.003125)
     truth = p_m71_prior(H, 0, 100, counts_rate=0.003125)
