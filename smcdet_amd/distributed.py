@@ -167,3 +167,46 @@ class ShardedBatchSMC:
     def gather_results(self, dst=0):
         return gather_tile_results(self.batch.results(), self.num_images, None, self.rank,
                                    self.world_size, dst=dst, group=self.group)
+
+
+class ShardedMCMC:
+    """MHsampler (the reference's MCMC baseline, experiments/m71/run_mcmc.py)
+    over this rank's contiguous slice of B independent cutouts [B, H, W]: one
+    chain launch per rank (MHsampler.from_tiles), no collective until the
+    end-of-run gather of the kept samples ([B, M, ...] on `dst`)."""
+
+    def __init__(self, images, Prior, ImageModel, locs_stdev, fluxes_stdev,
+                 flux_detection_threshold, num_samples_total, num_samples_burnin,
+                 keep_every_k=1, *, seed=None, device=None, group=None, **mh_kwargs):
+        from .sampler import MHsampler
+        self.rank, self.world_size = world()
+        self.group = group
+        self.num_images = images.shape[0]
+        self.start, self.stop = shard_tiles(self.num_images, self.world_size, self.rank)
+        if self.stop <= self.start:
+            raise ValueError(f"rank {self.rank} has no images ({self.num_images} images, "
+                             f"{self.world_size} ranks)")
+        seed = None if seed is None else int(seed) * 1000003 + self.rank
+        b = self.stop - self.start
+        H = images.shape[-1]
+        tiles = images[self.start:self.stop].reshape(1, b, H, H)
+        self.sampler = MHsampler.from_tiles(
+            tiles, Prior, ImageModel, locs_stdev, fluxes_stdev, flux_detection_threshold,
+            num_samples_total, num_samples_burnin, keep_every_k, seed=seed, device=device,
+            **mh_kwargs)
+
+    def run(self):
+        self.sampler.run()
+        return self
+
+    def local_results(self):
+        """Per-image kept samples in the run_mcmc.py layout: counts [b, M],
+        locs [b, M, S, 2], fluxes [b, M, S], acc_rate [b]."""
+        s = self.sampler
+        acc = s.accept.float().reshape(s.accept.shape[1], -1).mean(-1)
+        return {"counts": s.counts[0], "locs": s.locs[0], "fluxes": s.fluxes[0],
+                "pruned_counts": s.pruned_counts[0], "acc_rate": acc}
+
+    def gather_results(self, dst=0):
+        return gather_tile_results(self.local_results(), self.num_images, None, self.rank,
+                                   self.world_size, dst=dst, group=self.group)

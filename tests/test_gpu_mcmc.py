@@ -152,3 +152,23 @@ def test_mh_chain_poisson_many_chains_vs_oracle():
         same = (ga[:, :, c] == oacc).all(-1)
         np.testing.assert_allclose(gl[:, :, c][same], ol[same], rtol=0, atol=1e-3)
     assert ok / C > 0.99
+
+
+def test_sharded_mcmc_single_rank_equals_mhsampler():
+    """ShardedMCMC (smcdet_amd.distributed) on one rank is MHsampler.from_tiles
+    over all cutouts, with the per-image results in run_mcmc.py's layout."""
+    from smcdet_amd.distributed import ShardedMCMC
+    from smcdet_amd.sampler import MHsampler
+    d = golden("mcmc_m71_tiles.npz")
+    imgs = torch.as_tensor(tiles_of(d["image"], 8), device=DEV).reshape(4, 8, 8)
+    args = (p_m71_prior(8, 3, 3), p_m71_model(8), 0.1, 2.5, M71["flux_detection_threshold"],
+            400, 100, 3)
+    sh = ShardedMCMC(imgs, *args, seed=7, print_every=10 ** 9).run()
+    res = sh.gather_results()
+    ref = MHsampler.from_tiles(imgs.reshape(1, 4, 8, 8), *args, seed=7 * 1000003,
+                               print_every=10 ** 9)
+    ref.run()
+    M = (400 - 100 + 2) // 3
+    assert tuple(res["locs"].shape) == (4, M, 3, 2)
+    assert torch.equal(res["locs"], ref.locs[0]) and torch.equal(res["fluxes"], ref.fluxes[0])
+    assert tuple(res["acc_rate"].shape) == (4,)
