@@ -29,6 +29,12 @@ from . import _hip
 from ._rng import PhiloxStream
 
 
+def _scalar_or_tiles(v):
+    """.item() as the reference prints it for a single tile; the per-tile
+    values for a tiled image (where the reference's .item() raises)."""
+    return v.item() if v.numel() == 1 else v.cpu()
+
+
 class SMCsampler(object):
     def __init__(self, image, tile_dim, Prior, ImageModel, MutationKernel, num_catalogs,
                  ess_threshold_prop, resample_method, flux_detection_threshold, max_smc_iters,
@@ -471,9 +477,9 @@ class SMCsampler(object):
         print(vals.cpu())
         print((cnts / self.pruned_counts.shape[-1]).round(decimals=3).cpu(), "\n")
         print("posterior mean total intrinsic flux (including undetectable and/or in padding) =",
-              f"{self.posterior_mean_total_flux(self.fluxes).item()}\n")
+              f"{_scalar_or_tiles(self.posterior_mean_total_flux(self.fluxes))}\n")
         print("posterior mean total intrinsic flux of detectable stars within image boundary =",
-              f"{self.posterior_mean_total_flux(self.pruned_fluxes).item()}\n")
+              f"{_scalar_or_tiles(self.posterior_mean_total_flux(self.pruned_fluxes))}\n")
         print(f"number of unique catalogs = {self.fluxes[0, 0].sum(-1).unique(dim=0).shape[0]}")
 
     # ------------------------------------------------------------ checkpoint
