@@ -24,7 +24,8 @@
 //     change is evaluated in a cancellation-free form (pix_delta, device.h)
 //     whose error scales with the change, not with the absolute terms.  (Mode SMCDET_MH_FULL_RECOMPUTE instead
 //     re-renders every source each step, as the reference does.)
-//   * accept iff U <= min(1, exp(log alpha)) (kernel.py:114-116).
+//   * accept iff U <= min(1, exp(log alpha)) (kernel.py:114-116), evaluated
+//     as log alpha >= log U with log U precomputed per proposal batch.
 // The rate image comes from the ancestor's persisted image (rate_in) or a
 // fresh render; the returned loglik_out is summed over the final rate image
 // (fresh full render in FULL_RECOMPUTE mode).  The union-window positions run
@@ -335,7 +336,7 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
   // (lanes 3b+d); bfl = floor(current) | floor(proposed) << 16 (lanes 3b, 3b+1);
   // lane 3b+2: bampo/bampn = rate amplitudes g f psf_scale of the current /
   // proposed flux, bdp = prior term, bhs = summed Hastings term
-  float bmu = 0.f, bampo = 0.f, bampn = 0.f, bdp = 0.f, bhs = 0.f;
+  float bmu = 0.f, bampo = 0.f, bampn = 0.f, bdp = 0.f, bhs = 0.f, blu = 0.f;
   int bfl = 0;
   unsigned bmg = 1u;  // lane 3b+1: ceil(65536 / union-window width), for q / bw
   int bj = 0, batch_k0 = 0, batch_n = 0;
@@ -379,7 +380,10 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
     bdp = ((float)j < count) ? -a.pr.ap1 * (blf - lf_cur) : 0.0f;
     const float hd0 = __shfl(bhd, max(lane - 2, 0), kWave);
     const float hd1 = __shfl(bhd, max(lane - 1, 0), kWave);
-    bhs = hd0 + hd1 + bhd;
+    // log alpha = (Hastings + prior term) + tau * dll, accepted iff it is >= log U
+    // (U <= min(1, exp(log alpha)) for U in [0, 1); nan rejects)
+    bhs = (hd0 + hd1 + bhd) + bdp;
+    blu = fast_log(__shfl(ru4, kl, kWave));
     bj = j;
     batch_k0 = k0;
     batch_n = n_;
@@ -415,7 +419,6 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
       b = 0;
       j = readlane(bj, 0);
     }
-    const float uacc = readlane(ru4, kl);
     // the batch entry is current (its source was not moved since the batch)
     Proposal P;
     P.j = j;
@@ -424,8 +427,8 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
     P.hn = readlane(bx, 3 * b);
     P.wn = readlane(bx, 3 * b + 1);
     P.fn = readlane(bx, 3 * b + 2);
-    P.hast = readlane(bhs, 3 * b + 2);
-    const float dprior = readlane(bdp, 3 * b + 2);
+    P.hast = readlane(bhs, 3 * b + 2);  // Hastings + prior terms
+    const float log_u = readlane(blu, 3 * b + 2);
     // rate contributions g*f*psf, the psf normalisation folded into the amplitude
     const float amp_o = readlane(bampo, 3 * b + 2), amp_n = readlane(bampn, 3 * b + 2);
 
@@ -590,10 +593,8 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
     }
 
     // ---- accept / reject (kernel.py:114-128) ----------------------------------
-    const float loga = dprior + tau * dll + P.hast;
-    const float e = fast_exp(loga);
-    const float alpha = e > 1.0f ? 1.0f : e;  // clamp(max=1) keeps NaN
-    accept = __builtin_amdgcn_readfirstlane((uacc <= alpha) ? 1 : 0);
+    const float loga = fmaf(tau, dll, P.hast);
+    accept = __builtin_amdgcn_readfirstlane((loga >= log_u) ? 1 : 0);
 #ifdef SMCDET_TRACE
     tr_acc += accept;
 #endif
