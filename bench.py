@@ -263,10 +263,13 @@ def build_sampler(args, dev, rank):
                             "systematic", p["flux_detection_threshold"], 10 ** 9, 10 ** 9,
                             seed=12345 + rank, device=dev)
     NS = smax + 1
-    return cs.sampler, cs.MutationKernel, B * NS * Np * K, images[0], dict(
+    # the count-0 stratum has no source to move (its MH launch does no work):
+    # only the NS - 1 strata with s >= 1 make particle-steps
+    return cs.sampler, cs.MutationKernel, B * (NS - 1) * Np * K, images[0], dict(
         workload=f"C5: CS-SMC over {B} x 8x8 M71 tiles/GPU, counts 0..{smax} "
-                 f"({NS} strata as tiles, S={smax}), N={Np} per count, {K} MH iters per SMC step, "
-                 "systematic, rho=0.5", tiles_per_gpu=B, particles=Np * NS, tile=H, sources=smax,
+                 f"({NS} strata as tiles, S={smax}; particle-steps counted over the {NS - 1} strata "
+                 f"with s >= 1), N={Np} per count, {K} MH iters per SMC step, systematic, rho=0.5",
+        tiles_per_gpu=B, particles=Np * NS, tile=H, sources=smax,
         mh_iters=K, kernel=args.kernel)
 
 

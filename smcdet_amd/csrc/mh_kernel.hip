@@ -194,8 +194,24 @@ __device__ __forceinline__ f2 position_delta2(const DevModel& m, const float* xs
 // PPL = 0: LDS render (larger tiles)
 // PAIRED: union-window positions two per lane in packed arithmetic (default);
 // false: one per lane (SMCDET_MH_SCALAR_SLOTS, for A/B timing).
+// Small tiles (PPL == 1: H*W <= 64, e.g. the 8x8 M71 cutouts) never need more
+// than one union-window slot (npos <= H*W): only that path is compiled, which
+// fits the kernel in 72 VGPRs (3 spilled) and so runs 7 waves per SIMD instead
+// of 4 -- the per-iteration control of these short iterations is
+// latency-bound.  Same-box A/B (C4, MH launch): 4 waves + all slot paths
+// 5.93 ms; 1-slot path at 4 waves 5.33; 6 waves (80 VGPRs, no spill) 5.17;
+// 7 waves 5.11; 8 waves (64 VGPRs, 15 spilled) 5.62.
+#ifndef SMCDET_SMALL_TILE_WAVES
+#define SMCDET_SMALL_TILE_WAVES 7
+#endif
+template <int PPL>
+constexpr int mh_waves_per_eu() { return PPL == 1 ? SMCDET_SMALL_TILE_WAVES : 4; }
+template <int PPL>
+constexpr int mh_slots() { return PPL == 1 ? 1 : kSlots; }
+
 template <int MODEL, bool REPLAY, bool FULL, int PPL, bool PAIRED>
-__global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
+__global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_kernel(MhArgs a) {
+  constexpr int NSL = mh_slots<PPL>();
   extern __shared__ float smem[];
   __shared__ int wg_acc, wg_done;  // last-iteration accepts / finished waves of this workgroup
   if (a.go && *a.go == 0) return;  // speculatively enqueued sweep that must not run
@@ -435,8 +451,8 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
     // ---- likelihood difference -----------------------------------------------
     float dll;
     double new_ll = 0.0;
-    float s_lam[kSlots];
-    int s_pix[kSlots];
+    float s_lam[NSL];
+    int s_pix[NSL];
     int npos = 0, bw = 1, r0 = 0, c0 = 0, nslots = 0;
     if constexpr (FULL) {
       const float ch = lane == P.j ? P.hn : sh, cw = lane == P.j ? P.wn : sw;
@@ -553,7 +569,9 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
       using Win = std::true_type;
       using Same = std::false_type;
       float dsum = 0.f;
-      if (nslots == 0) {
+      if constexpr (NSL == 1) {
+        if (nslots == 1) dsum = same ? slots(I1{}, Same{}) : slots(I1{}, Win{});
+      } else if (nslots == 0) {
       } else if (PAIRED && nslots == 1) {
         dsum = same ? pairs(I0{}, One{}, Same{}) : pairs(I0{}, One{}, Win{});
       } else if (PAIRED && nslots == 2) {
@@ -575,7 +593,7 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
       } else {
         dsum = slots(I8{}, Win{});
       }
-      if (nslots > 5) {
+      if (NSL > 1 && nslots > 5) {
         // rare: a union window larger than the register slots (a jump of several px)
         if (npos > kSlots * kWave) {
           const float inv_bw = 1.0f / (float)bw;
@@ -603,9 +621,9 @@ __global__ __launch_bounds__(kMhBlock, 4) void mh_sweep_kernel(MhArgs a) {
         cur_ll = new_ll;
       } else {
 #pragma unroll
-        for (int i = 0; i < kSlots; ++i)
+        for (int i = 0; i < NSL; ++i)
           if (i < nslots) lam[s_pix[i]] = s_lam[i];
-        if (npos > kSlots * kWave) {
+        if (NSL > 1 && npos > kSlots * kWave) {
           const int flh = readlane(bfl, 3 * b), flw = readlane(bfl, 3 * b + 1);
           const int fh0 = (int)(int16_t)(flh & 0xffff), fh1 = flh >> 16;
           const int fw0 = (int)(int16_t)(flw & 0xffff), fw1 = flw >> 16;
