@@ -15,7 +15,7 @@ for r in $(seq 1 $ROUNDS); do
       rc=$?
       if [ $rc -ne 0 ]; then echo "$wl $v rc=$rc"; tail -5 $out.log; exit $rc; fi
       tail -1 $out.log > $out
-      python -c "import json; d=json.load(open('$out')); print('$wl', '$ENVVAR=$v', 'r$r', '%.4g' % d['value'], 'step_ms %.4f' % d['ms_per_step'], 'mh_ms %.4f' % d['roofline']['kernel_ms'])"
+      python -c "import json; d=json.load(open('$out')); print('$wl', '$ENVVAR=$v', 'r$r', '%.4g' % d['value'], 'step_ms %.4f' % d['ms_per_step'], 'mh_ms', d.get('roofline', {}).get('kernel_ms'))"
     done
   done
 done

@@ -21,6 +21,7 @@ namespace smcdet {
 
 constexpr int kChainWaves = 4;
 constexpr int kChainBlock = kChainWaves * kWave;
+constexpr int kChainBatch = 8;  // proposals computed together (6 lanes each)
 
 struct ChainArgs {
   DevModel m;
@@ -91,10 +92,6 @@ __global__ __launch_bounds__(kChainBlock, 4) void mh_chain_kernel(ChainArgs a) {
   };
   if (a.k_begin == 0) record(0);
 
-  const int d = lane % 3;  // proposal dimension of this lane (lanes 3.. replicate 0..2)
-  const float dsig = d < 2 ? a.sl : a.sf, drs = d < 2 ? a.rsl : a.rsf;
-  const float dlb = d == 0 ? a.lb_h : (d == 1 ? a.lb_w : a.lb_f);
-  const float dub = d == 0 ? a.ub_h : (d == 1 ? a.ub_w : a.ub_f);
   const float gs = m.g * (poisson ? psf_scale<SMCDET_MODEL_POISSON>(m)
                                   : psf_scale<SMCDET_MODEL_M71>(m));
   const int K = a.total - 1;
@@ -125,21 +122,62 @@ __global__ __launch_bounds__(kChainBlock, 4) void mh_chain_kernel(ChainArgs a) {
     }
   };
 
+  // ---- proposals and Hastings terms (sampler.py:435-495), batched off the
+  // chain's critical path: lane 6b+r computes dimension r % 3 of iteration
+  // batch_k0 + b (r < 3: cdf at the lower bound, r >= 3: at the upper bound,
+  // exchanged within the group), from the state at batch time.  An entry goes
+  // stale only if an earlier accepted iteration of the batch moved the same
+  // source (tracked in `dirty`); the batch is then recomputed from there.
+  // Each proposal is the same arithmetic on the same inputs as one computed
+  // at its own iteration.
+  const int gb = lane / 6, gr = lane - 6 * gb, gd = gr % 3;
+  const float gsig = gd < 2 ? a.sl : a.sf, grs = gd < 2 ? a.rsl : a.rsf;
+  const float glb = gd == 0 ? a.lb_h : (gd == 1 ? a.lb_w : a.lb_f);
+  const float gub = gd == 0 ? a.ub_h : (gd == 1 ? a.ub_w : a.ub_f);
+  float bcur = 0.f, bxn = 0.f, bqf = 0.f, bqr = 0.f;
+  int bj = 0, batch_k0 = 0, batch_n = 0;
+  uint64_t dirty = 0;
+  auto compute_batch = [&](int k0) {
+    const int off = (k0 - a.k_begin) & 63;
+    const int n_ = min(min(kChainBatch, kWave - off), a.k_end - k0);
+    const int b = min(gb, n_ - 1);
+    const int kl = off + b;
+    const int j = a.r_comp ? __shfl(rcomp, kl, kWave)
+                           : min((int)(__shfl(ru0, kl, kWave) * (float)S), S - 1);
+    const float u1 = __shfl(ru1, kl, kWave), u2 = __shfl(ru2, kl, kWave);
+    const float u3 = __shfl(ru3, kl, kWave);
+    const float ud = gd == 0 ? u1 : (gd == 1 ? u2 : u3);
+    const float h = __shfl(sh, j, kWave), w = __shfl(sw, j, kWave), f = __shfl(sfx, j, kWave);
+    const float cur = gd == 0 ? h : (gd == 1 ? w : f);
+    const int src = 6 * b + gd;
+    const TnBox bc = t_box_group(cur, grs, glb, gub, gr, src);
+    const float xn = t_sample_box(cur, gsig, glb, gub, ud, bc);
+    bqf = t_logprob_box(xn, cur, gsig, bc);
+    bqr = t_logprob_box(cur, xn, gsig, t_box_group(xn, grs, glb, gub, gr, src));
+    bxn = xn;
+    bcur = cur;
+    bj = j;
+    batch_k0 = k0;
+    batch_n = n_;
+    dirty = 0;
+  };
+
   for (int k = a.k_begin; k < a.k_end; ++k) {
     const int kl = (k - a.k_begin) & 63;
     if (kl == 0) refill(k);
-    const int j = a.r_comp ? readlane(rcomp, kl) : min((int)(readlane(ru0, kl) * (float)S), S - 1);
+    if (k >= batch_k0 + batch_n) compute_batch(k);
+    int b = k - batch_k0;
+    int j = readlane(bj, 6 * b);
+    if ((dirty >> j) & 1ull) {
+      compute_batch(k);
+      b = 0;
+      j = readlane(bj, 0);
+    }
     const float uacc = readlane(ru4, kl);
-    const float ud = d == 0 ? readlane(ru1, kl) : (d == 1 ? readlane(ru2, kl) : readlane(ru3, kl));
-    const float h = readlane(sh, j), w = readlane(sw, j), f = readlane(sfx, j);
-
-    // ---- proposal and Hastings terms (sampler.py:435-495) -------------------
-    const float cur = d == 0 ? h : (d == 1 ? w : f);
-    const TnBox bc = t_box_lanes(cur, drs, dlb, dub, lane);
-    const float xn = t_sample_box(cur, dsig, dlb, dub, ud, bc);
-    const float q_fwd = t_logprob_box(xn, cur, dsig, bc);
-    const float q_rev = t_logprob_box(cur, xn, dsig, t_box_lanes(xn, drs, dlb, dub, lane));
-    const float hn = readlane(xn, 0), wn = readlane(xn, 1), fn = readlane(xn, 2);
+    const float h = readlane(bcur, 6 * b), w = readlane(bcur, 6 * b + 1);
+    const float f = readlane(bcur, 6 * b + 2);
+    const float hn = readlane(bxn, 6 * b), wn = readlane(bxn, 6 * b + 1);
+    const float fn = readlane(bxn, 6 * b + 2);
 
     // ---- delta log-likelihood over the new window and the old-only positions
     const Window qo = window_of(m, h, w), qn = window_of(m, hn, wn);
@@ -189,9 +227,9 @@ __global__ __launch_bounds__(kChainBlock, 4) void mh_chain_kernel(ChainArgs a) {
     const float dprior = active ? -a.pr.ap1 * (fast_log(fnt) - fast_log(ft)) : 0.f;
     const bool outside = hn >= a.pr.hi_h || wn >= a.pr.hi_w || hn < a.pr.lo || wn < a.pr.lo;
     const float la = (dprior + dll) +
-                     (((readlane(q_rev, 0) - readlane(q_fwd, 0)) +
-                       (readlane(q_rev, 1) - readlane(q_fwd, 1))) +
-                      (readlane(q_rev, 2) - readlane(q_fwd, 2)));
+                     (((readlane(bqr, 6 * b) - readlane(bqf, 6 * b)) +
+                       (readlane(bqr, 6 * b + 1) - readlane(bqf, 6 * b + 1))) +
+                      (readlane(bqr, 6 * b + 2) - readlane(bqf, 6 * b + 2)));
     const float e = expf(la);
     const float alpha = e > 1.0f ? 1.0f : e;
     const int accept = __builtin_amdgcn_readfirstlane((!outside && uacc <= alpha) ? 1 : 0);
@@ -209,6 +247,7 @@ __global__ __launch_bounds__(kChainBlock, 4) void mh_chain_kernel(ChainArgs a) {
       sh = writelane(hn, j, sh);
       sw = writelane(wn, j, sw);
       sfx = writelane(fn, j, sfx);
+      dirty |= 1ull << j;
     }
     wave_sync();
     if (a.accept_out && lane == 0) a.accept_out[pid * (size_t)K + k] = accept;

@@ -91,6 +91,19 @@ __device__ __forceinline__ TnBox t_box_lanes(float mu, float rsig, float lb, flo
   b.logZ = nan_to_num(logf(__shfl(c, d + 3, kWave) - b.cdf_lb), 0.0f);
   return b;
 }
+// The same for proposal groups of 6 lanes (lane r of a group: r < 3 -> lb,
+// r >= 3 -> ub of dimension r % 3): src = the group's lane of dimension d with
+// r < 3.  Same arithmetic as t_box_lanes.
+__device__ __forceinline__ TnBox t_box_group(float mu, float rsig, float lb, float ub, int r,
+                                             int src) {
+#pragma clang fp contract(off)
+  const float v = r >= 3 ? ub : lb;
+  const float c = t_cdf(v, mu, rsig);
+  TnBox b;
+  b.cdf_lb = __shfl(c, src, kWave);
+  b.logZ = nan_to_num(logf(__shfl(c, src + 3, kWave) - b.cdf_lb), 0.0f);
+  return b;
+}
 // t_sample / t_logprob with the box quantities of t_box_lanes
 __device__ __forceinline__ float t_sample_box(float mu, float sig, float lb, float ub, float u,
                                               const TnBox& b) {
