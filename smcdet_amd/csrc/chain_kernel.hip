@@ -205,7 +205,10 @@ __global__ __launch_bounds__(kChainBlock, 4) void mh_chain_kernel(ChainArgs a) {
                       : pix_delta<SMCDET_MODEL_M71>(m, xs[p], 0.f, lo, dl);
       scr[i] = lo + dl;
     }
-    for (int i = lane; i < qo.npos; i += kWave) {
+    // old-only positions exist unless the old window's clipped box lies inside
+    // the new window (same anchors, or both cover a small tile): skip the walk
+    const bool old_only = has_old_only(m, qo, qn);
+    for (int i = lane; old_only && i < qo.npos; i += kWave) {
       int ph, pw;
       window_pos(qo, i, ph, pw);
       if (in_window(m, qn.fh, qn.fw, ph, pw)) continue;
@@ -239,7 +242,7 @@ __global__ __launch_bounds__(kChainBlock, 4) void mh_chain_kernel(ChainArgs a) {
         window_pos(qn, i, ph, pw);
         lam[ph * m.W + pw] = scr[i];
       }
-      for (int i = lane; i < qo.npos; i += kWave) {
+      for (int i = lane; old_only && i < qo.npos; i += kWave) {
         int ph, pw;
         window_pos(qo, i, ph, pw);
         if (!in_window(m, qn.fh, qn.fw, ph, pw)) lam[ph * m.W + pw] = scr[a.W2 + i];

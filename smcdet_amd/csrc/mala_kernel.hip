@@ -241,7 +241,9 @@ __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
       pgw = fmaf(ed, dwn, pgw);
     }
     // old window positions outside the new window: the source's rate leaves
-    for (int i = lane; i < qo.npos; i += kWave) {
+    // (no walk when the old window's clipped box lies inside the new window)
+    const bool old_only = has_old_only(m, qo, qn);
+    for (int i = lane; old_only && i < qo.npos; i += kWave) {
       int ph, pw;
       window_pos(qo, i, ph, pw);
       if (in_window(m, qn.fh, qn.fw, ph, pw)) continue;
@@ -298,7 +300,7 @@ __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
         window_pos(qn, i, ph, pw);
         lam[ph * m.W + pw] = scr[i];
       }
-      for (int i = lane; i < qo.npos; i += kWave) {
+      for (int i = lane; old_only && i < qo.npos; i += kWave) {
         int ph, pw;
         window_pos(qo, i, ph, pw);
         if (!in_window(m, qn.fh, qn.fw, ph, pw)) lam[ph * m.W + pw] = scr[a.W2 + i];

@@ -150,5 +150,14 @@ __device__ __forceinline__ bool in_window(const DevModel& m, int fh, int fw, int
   const unsigned span = 2u * (unsigned)m.R;
   return (unsigned)(ph - fh + m.R) <= span && (unsigned)(pw - fw + m.R) <= span;
 }
+// true if window qo has positions outside window qn: false when qo's clipped
+// box lies inside qn's (unclipped) window -- same anchors, or both windows
+// covering a small tile -- so the old-only walks can be skipped
+__device__ __forceinline__ bool has_old_only(const DevModel& m, const Window& qo,
+                                             const Window& qn) {
+  return qo.npos > 0 &&
+         !(qo.r0 >= qn.fh - m.R && min(qo.fh + m.R, m.H - 1) <= qn.fh + m.R &&
+           qo.c0 >= qn.fw - m.R && min(qo.fw + m.R, m.W - 1) <= qn.fw + m.R);
+}
 
 }  // namespace smcdet
