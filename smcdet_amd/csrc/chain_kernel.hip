@@ -183,6 +183,10 @@ __global__ __launch_bounds__(kChainBlock, 4) void mh_chain_kernel(ChainArgs a) {
     const Window qo = window_of(m, h, w), qn = window_of(m, hn, wn);
     const float amp_o = gs * f, amp_n = gs * fn;
     float dsum = 0.f;
+    // the moved rates of the lane's first new-window position stay in
+    // registers (all of them on tiles of <= 64 pixels); further ones go to scr
+    float v0 = 0.f;
+    int p0 = 0;
     for (int i = lane; i < qn.npos; i += kWave) {
       int ph, pw;
       window_pos(qn, i, ph, pw);
@@ -203,7 +207,12 @@ __global__ __launch_bounds__(kChainBlock, 4) void mh_chain_kernel(ChainArgs a) {
       const float lo = lam[p];
       dsum += poisson ? pix_delta<SMCDET_MODEL_POISSON>(m, xs[p], lg[p], lo, dl)
                       : pix_delta<SMCDET_MODEL_M71>(m, xs[p], 0.f, lo, dl);
-      scr[i] = lo + dl;
+      if (i < kWave) {
+        v0 = lo + dl;
+        p0 = p;
+      } else {
+        scr[i] = lo + dl;
+      }
     }
     // old-only positions exist unless the old window's clipped box lies inside
     // the new window (same anchors, or both cover a small tile): skip the walk
@@ -237,7 +246,8 @@ __global__ __launch_bounds__(kChainBlock, 4) void mh_chain_kernel(ChainArgs a) {
     const float alpha = e > 1.0f ? 1.0f : e;
     const int accept = __builtin_amdgcn_readfirstlane((!outside && uacc <= alpha) ? 1 : 0);
     if (accept) {
-      for (int i = lane; i < qn.npos; i += kWave) {
+      if (lane < qn.npos) lam[p0] = v0;
+      for (int i = lane + kWave; i < qn.npos; i += kWave) {
         int ph, pw;
         window_pos(qn, i, ph, pw);
         lam[ph * m.W + pw] = scr[i];
