@@ -138,7 +138,10 @@ __device__ __forceinline__ Window window_of(const DevModel& m, float h, float w)
   const int r1 = min(q.fh + m.R, m.H - 1), c1 = min(q.fw + m.R, m.W - 1);
   q.bw = max(c1 - q.c0 + 1, 1);
   q.npos = (r1 >= q.r0 && c1 >= q.c0) ? (r1 - q.r0 + 1) * (c1 - q.c0 + 1) : 0;
-  q.inv_bw = 1.0f / (float)q.bw;
+  // v_rcp_f32 (1 ulp) instead of an IEEE division on the chain's critical path:
+  // window_pos's floor((i + 0.5) / bw) stays exact, since (i + 0.5) / bw is at
+  // least 0.5 / bw from an integer and the rcp error is ~1e-7 relative
+  q.inv_bw = __builtin_amdgcn_rcpf((float)q.bw);
   return q;
 }
 __device__ __forceinline__ void window_pos(const Window& q, int i, int& ph, int& pw) {
