@@ -71,6 +71,8 @@ struct MalaArgs {
   const float* r_uacc;
 };
 
+constexpr int kKeep = 5;  // register-resident new-window slots (5*64 >= 17*17)
+
 template <int MODEL, bool REPLAY>
 __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
   extern __shared__ float smem[];
@@ -218,7 +220,9 @@ __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
     const Window qn = window_of(m, hn, wn);
     const float amp_o = gs * f, amp_n = gs * fn;
     float dsum = 0.f, pgh = 0.f, pgw = 0.f, pgf = 0.f;
-    for (int i = lane; i < qn.npos; i += kWave) {
+    // one new-window position: accumulates the delta and the gradient, returns
+    // the moved rate (same per-lane order over i as a plain strided loop)
+    auto new_pos = [&](int i, int& p) -> float {
       int ph, pw;
       window_pos(qn, i, ph, pw);
       const float fph = (float)ph + 0.5f, fpw = (float)pw + 0.5f;
@@ -228,17 +232,32 @@ __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
       float psi_o = 0.f;
       if (in_window(m, qo.fh, qo.fw, ph, pw)) psi_o = psc[(ph - qo.r0) * qo.bw + (pw - qo.c0)];
       const float dl = fmaf(amp_n, psi_n, -amp_o * psi_o);
-      const int p = ph * m.W + pw;
+      p = ph * m.W + pw;
       const float lo = lam[p], x = xs[p];
       const float lgx = (MODEL == SMCDET_MODEL_POISSON) ? lg[p] : 0.0f;
       dsum += pix_delta<MODEL>(m, x, lgx, lo, dl);
       const float l1 = lo + dl;
-      scr[i] = l1;
       const float e = dll_drate<MODEL>(m, x, l1);
       pgf = fmaf(e, psi_n, pgf);
       const float ed = e * dpsi;
       pgh = fmaf(ed, dhn, pgh);
       pgw = fmaf(ed, dwn, pgw);
+      return l1;
+    };
+    // the first kKeep positions per lane keep their moved rates in registers
+    // (a whole 17x17 window), further ones go to the LDS scratch
+    float kv[kKeep];
+    int kp[kKeep];
+#pragma unroll
+    for (int s_ = 0; s_ < kKeep; ++s_) {
+      const int i = lane + s_ * kWave;
+      kp[s_] = 0;
+      kv[s_] = 0.f;
+      if (i < qn.npos) kv[s_] = new_pos(i, kp[s_]);
+    }
+    for (int i = lane + kKeep * kWave; i < qn.npos; i += kWave) {
+      int p;
+      scr[i] = new_pos(i, p);
     }
     // old window positions outside the new window: the source's rate leaves
     // (no walk when the old window's clipped box lies inside the new window)
@@ -295,7 +314,10 @@ __global__ __launch_bounds__(kMalaBlock, 4) void mala_sweep_kernel(MalaArgs a) {
     const float alpha = e > 1.0f ? 1.0f : e;  // clamp(max=1) keeps nan
     accept = __builtin_amdgcn_readfirstlane((!outside && uacc <= alpha) ? 1 : 0);
     if (accept) {
-      for (int i = lane; i < qn.npos; i += kWave) {
+#pragma unroll
+      for (int s_ = 0; s_ < kKeep; ++s_)
+        if (lane + s_ * kWave < qn.npos) lam[kp[s_]] = kv[s_];
+      for (int i = lane + kKeep * kWave; i < qn.npos; i += kWave) {
         int ph, pw;
         window_pos(qn, i, ph, pw);
         lam[ph * m.W + pw] = scr[i];
