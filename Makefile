@@ -7,11 +7,18 @@ SRCS := $(CSRC)/common.hip $(CSRC)/model_kernels.hip $(CSRC)/mh_kernel.hip $(CSR
 HDRS := $(CSRC)/device.h $(CSRC)/render.h $(CSRC)/mcmc.h include/smcdet_hip.h
 OBJS := $(SRCS:.hip=.o)
 LIB := smcdet_amd/libsmcdet_hip.so
+# build provenance: sha1 of the sources in this order (smcdet_amd/_hip.py
+# SOURCES recomputes it and refuses a library built from other sources)
+SRC_HASH := $(shell cat $(SRCS) $(HDRS) | sha1sum | cut -c1-40)
 
 all: $(LIB) oracle
 
 $(CSRC)/%.o: $(CSRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# the hash is compiled into common.o, so it depends on every source
+$(CSRC)/common.o: $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -DSMCDET_SRC_HASH=\"$(SRC_HASH)\" -c $(CSRC)/common.hip -o $@
 
 $(LIB): $(OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJS)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 9
+#define SMCDET_ABI_VERSION 10
 
 /* status codes */
 #define SMCDET_OK 0
@@ -58,6 +58,12 @@ extern "C" {
 /* independent stopping: tiles whose temperature is already 1 are not mutated
  * (their particles are only gathered through `ancestors`) */
 #define SMCDET_MH_SKIP_DONE 4u
+
+/* (no flag) A location proposal clamped onto the prior box's upper edge
+ * (distributions.py:48) has log prior -inf (Uniform.log_prob(high),
+ * prior.py:73) and is rejected; as in the reference, whose cached log target
+ * then becomes -inf * 0 = NaN (kernel.py:125), the particle also rejects every
+ * remaining proposal of that sweep. */
 
 /* temper_reweight flags */
 /* independent stopping: a tile that entered at temperature 1 keeps it (delta
@@ -119,6 +125,7 @@ typedef struct smcdet_mh_replay {
   const float* uacc;   /* [K,T,N]   */
 } smcdet_mh_replay_t;
 
+/* "smcdet_hip <version> (gfx950) src <sha1 of the library's sources>" */
 const char* smcdet_version(void);
 int32_t smcdet_abi_version(void);
 const char* smcdet_last_error(void);

@@ -241,9 +241,18 @@ int mh_oracle_sweep(const om_model_t* m, const om_prior_t* pr, const om_mh_t* mh
           ua = urand(&st);
         }
         const double oh = h[j], ow = w[j], of = f[j];
-        const double nh = tn_sample(oh, mh->sl, mh->lb_h, mh->ub_h, uh);
-        const double nw = tn_sample(ow, mh->sl, mh->lb_w, mh->ub_w, uw);
-        const double nf = tn_sample(of, mh->sf, mh->lb_f, mh->ub_f, uf);
+        /* proposals as the reference's float32 state holds them */
+        const double nh = (float)tn_sample(oh, mh->sl, mh->lb_h, mh->ub_h, uh);
+        const double nw = (float)tn_sample(ow, mh->sl, mh->lb_w, mh->ub_w, uw);
+        const double nf = (float)tn_sample(of, mh->sf, mh->lb_f, mh->ub_f, uf);
+        /* a location on the box's upper edge has log prior -inf
+         * (Uniform.log_prob(high), prior.py:73): rejected, and the reference's
+         * cached target becomes -inf * 0 = NaN (kernel.py:125), which rejects
+         * every remaining proposal of the sweep */
+        if (nh >= pr->loc_high_h || nw >= pr->loc_high_w) {
+          acc = 0;
+          break;
+        }
         /* Hastings: the Normal log-densities cancel; log-mass-in-box terms remain */
         const double hast = tn_logZ(oh, mh->sl, mh->lb_h, mh->ub_h) -
                             tn_logZ(nh, mh->sl, mh->lb_h, mh->ub_h) +

@@ -352,13 +352,16 @@ def log_target(tiled_image, counts, locs, fluxes, tau, prior, model, dtype=np.fl
 
 
 def mh_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mh,
-             comp, uloc, uflux, uacc, dtype=np.float64, trace=False):
+             comp, uloc, uflux, uacc, dtype=np.float64, trace=False, edge_freeze=True):
     """SingleComponentMH.run (kernel.py:26-130) with its draws given explicitly:
     comp [K,nH,nW,N] (the one-hot component of Multinomial.sample, :44),
     uloc [K,nH,nW,N,2] / uflux [K,nH,nW,N] (torch.rand of the truncated-normal
     proposals for the chosen component, :47-61), uacc [K,nH,nW,N] (:115).
     Returns (locs, fluxes, acc_rate_of_last_iteration [nH,nW]) and, with
-    trace=True, per-iteration log-alpha and accept flags."""
+    trace=True, per-iteration log-alpha and accept flags.  edge_freeze=False
+    caches the target with np.where instead of the reference's arithmetic
+    (no NaN after a rejected upper-edge proposal: what the reference would do
+    with torch.where as its MALA kernel caches, kernel.py:273)."""
     locs = np.array(locs, dtype=dtype)
     fluxes = np.array(fluxes, dtype=dtype)
     K = comp.shape[0]
@@ -373,8 +376,12 @@ def mh_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mh,
         j = comp[k][..., None]  # [nH,nW,N,1]
         lj = np.take_along_axis(locs, j[..., None].repeat(2, -1), axis=-2)[..., 0, :]
         fj = np.take_along_axis(fluxes, j, axis=-1)[..., 0]
+        # proposals are stored as the reference's float32 state holds them: a
+        # draw within half an ulp of the box's upper edge lands exactly on it
         lnew = tn_sample(lj, sl, lb_l, ub_l, uloc[k].astype(dtype))  # :47-52
         fnew = tn_sample(fj, sf, lb_f, ub_f, uflux[k].astype(dtype))  # :53-61
+        lnew = lnew.astype(np.float32).astype(dtype)
+        fnew = fnew.astype(np.float32).astype(dtype)
         pl = locs.copy()
         pf = fluxes.copy()
         np.put_along_axis(pl, j[..., None].repeat(2, -1), lnew[..., None, :], axis=-2)
@@ -390,7 +397,14 @@ def mh_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mh,
         accept = uacc[k].astype(dtype) <= alpha  # :115-116
         locs = np.where(accept[..., None, None], pl, locs)  # :118-122
         fluxes = np.where(accept[..., None], pf, fluxes)
-        cur_lt = np.where(accept, new_lt, cur_lt)  # :125
+        # :125 caches log_num_target * accept + log_denom_target * ~accept: a
+        # rejected -inf target (a location on the box's upper edge, log prior
+        # -inf) becomes NaN, and every later proposal of the particle is rejected
+        if edge_freeze:
+            with np.errstate(invalid="ignore"):
+                cur_lt = new_lt * accept + cur_lt * (~accept)
+        else:
+            cur_lt = np.where(accept, new_lt, cur_lt)
         if trace:
             loga_tr.append(loga)
             acc_tr.append(accept)

@@ -15,7 +15,8 @@ for r in $(seq 1 $ROUNDS); do
       lib=smcdet_amd/libsmcdet_hip.so
       [ "$tag" != cur ] && lib=smcdet_amd/libsmcdet_hip_$tag.so
       out=gpurun_out/ab/${wl}_${tag}_r$r.json
-      SMCDET_HIP_LIB=$PWD/$lib timeout -k 10 240 python bench.py --workload $wl --no-cpu-baseline \
+      # variants built elsewhere (e.g. an older commit) carry another source hash
+      SMCDET_ALLOW_STALE=1 SMCDET_HIP_LIB=$PWD/$lib timeout -k 10 240 python bench.py --workload $wl --no-cpu-baseline \
         --no-full-run ${BENCH_ARGS:-} > $out.log 2>&1
       rc=$?
       if [ $rc -ne 0 ]; then echo "$wl $tag rc=$rc"; tail -5 $out.log; exit $rc; fi

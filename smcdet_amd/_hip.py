@@ -23,6 +23,7 @@ SMCDET_RESAMPLE_SYSTEMATIC = 1
 SMCDET_MH_FULL_RECOMPUTE = 1
 SMCDET_MH_COMPONENT_BY_COUNT = 2
 SMCDET_MH_SKIP_DONE = 4
+ABI_VERSION = 10
 SMCDET_SMC_FREEZE_DONE = 1
 
 c_f = ctypes.c_float
@@ -89,9 +90,38 @@ EXPORTS = tuple(_SIGS)
 
 _lib = None
 
+# the library's sources in the Makefile's SRCS + HDRS order: their sha1 is
+# compiled into smcdet_version() ("src <sha1>")
+_REPO = os.path.dirname(_HERE)
+SOURCES = tuple(os.path.join(_REPO, p) for p in (
+    "smcdet_amd/csrc/common.hip", "smcdet_amd/csrc/model_kernels.hip",
+    "smcdet_amd/csrc/mh_kernel.hip", "smcdet_amd/csrc/mala_kernel.hip",
+    "smcdet_amd/csrc/chain_kernel.hip", "smcdet_amd/csrc/smc_kernels.hip",
+    "smcdet_amd/csrc/device.h", "smcdet_amd/csrc/render.h", "smcdet_amd/csrc/mcmc.h",
+    "include/smcdet_hip.h"))
+
+
+def source_hash():
+    """sha1 of SOURCES as they are on disk (None if any is missing)."""
+    import hashlib
+    h = hashlib.sha1()
+    for p in SOURCES:
+        if not os.path.exists(p):
+            return None
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def built_hash(L=None):
+    v = (L or lib()).smcdet_version().decode()
+    return v.rsplit("src ", 1)[-1] if "src " in v else None
+
 
 def lib():
-    """Load libsmcdet_hip.so once (raises if it is missing: there is no fallback)."""
+    """Load libsmcdet_hip.so once.  Raises if it is missing (there is no
+    fallback) or if it was built from other sources than the ones next to it
+    (a stale library; SMCDET_ALLOW_STALE=1 skips that check)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
@@ -103,6 +133,12 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
+        if os.environ.get("SMCDET_ALLOW_STALE") != "1":
+            src, built = source_hash(), built_hash(L)
+            if src is not None and built != src:
+                raise RuntimeError(
+                    f"smcdet_amd: {LIB_PATH} was built from sources with sha1 {built}, the "
+                    f"sources here hash to {src}: rebuild with `make`")
         _lib = L
     return _lib
 

@@ -16,6 +16,22 @@ def torch_seed() -> int:
     return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
 
 
+def rank_seed(seed, rank: int) -> int:
+    """Seed of rank `rank`'s streams in a sharded run.  The kernels key their
+    draws by the rank-local tile/particle index, so ranks must not share a
+    seed (under torchrun every rank's torch.manual_seed is usually the same).
+    Rank 0 keeps the base seed, so a one-rank shard reproduces the
+    single-process sampler with that seed; other ranks get a splitmix64 mix
+    of (base, rank).  seed None: the base comes from torch's generator."""
+    base = torch_seed() if seed is None else int(seed) & ((1 << 64) - 1)
+    if rank == 0:
+        return base
+    z = (base + 0x9E3779B97F4A7C15 * (rank + 1)) & ((1 << 64) - 1)
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & ((1 << 64) - 1)
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & ((1 << 64) - 1)
+    return (z ^ (z >> 31)) & ((1 << 63) - 1)
+
+
 class PhiloxStream:
     def __init__(self, seed: int | None = None):
         self.seed = torch_seed() if seed is None else int(seed) & ((1 << 64) - 1)

@@ -62,7 +62,9 @@ class BatchSMC(object):
         """Per-image results in the drivers' layout (run_smc.py:106-111,
         160-168): counts [B,N], locs [B,N,S,2], fluxes [B,N,S],
         posterior_predictive_total_flux [B,N], num_iters [B] (SMC iterations
-        until the image reached temperature 1), runtime [B] (the batch's wall
+        until the image reached temperature 1; an image that never did, within
+        max_smc_iters, gets the sampler's final `iter` = max_smc_iters + 1, what
+        the reference drivers save as sampler.iter), runtime [B] (the batch's wall
         time shared equally: the images ran together), plus log Z, final ESS
         and the pruned catalogs."""
         if not self.has_run:
@@ -72,7 +74,8 @@ class BatchSMC(object):
         pp = self.ImageModel.sample(s.locs, s.fluxes).sum([2, 3])   # [1,B,N]
         return {
             "runtime": torch.full((B,), self.runtime / B),
-            "num_iters": self._flat(s.iters_per_tile).to(torch.float32),
+            "num_iters": self._flat(torch.where(s.iters_per_tile < 0, int(s.iter),
+                                                s.iters_per_tile)).to(torch.float32),
             "counts": self._flat(s.counts),
             "locs": self._flat(s.locs),
             "fluxes": self._flat(s.fluxes),

@@ -120,7 +120,11 @@ int validate_prior(const smcdet_prior_t* p) {
 
 extern "C" {
 
-const char* smcdet_version(void) { return "smcdet_hip 0.1.0 (gfx950)"; }
+#ifndef SMCDET_SRC_HASH
+#define SMCDET_SRC_HASH "unknown"
+#endif
+// "src <sha1>": the sha1 of the library's sources (Makefile SRC_HASH)
+const char* smcdet_version(void) { return "smcdet_hip 0.2.0 (gfx950) src " SMCDET_SRC_HASH; }
 int32_t smcdet_abi_version(void) { return SMCDET_ABI_VERSION; }
 const char* smcdet_last_error(void) { return smcdet::g_err; }
 

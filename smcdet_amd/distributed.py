@@ -24,6 +24,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from ._rng import rank_seed
 from .sampler import SMCsampler
 
 
@@ -53,8 +54,12 @@ class TileShardedSMC:
     def __init__(self, image, tile_dim, Prior, ImageModel, MutationKernel, num_catalogs,
                  ess_threshold_prop, resample_method, flux_detection_threshold, max_smc_iters,
                  print_every=10 ** 9, *, lockstep=False, seed=None, device=None, group=None,
-                 **sampler_kwargs):
-        self.rank, self.world_size = world()
+                 rank=None, world_size=None, **sampler_kwargs):
+        # rank / world_size default to the process group's (explicit values let
+        # one process build any rank's shard, e.g. to check sharded == unsharded)
+        r, w = world()
+        self.rank = r if rank is None else int(rank)
+        self.world_size = w if world_size is None else int(world_size)
         self.group = group
         self.lockstep = lockstep
         tiles = split_tiles(image, tile_dim)
@@ -65,7 +70,7 @@ class TileShardedSMC:
         if local.shape[0] == 0:
             raise ValueError(f"rank {self.rank} has no tiles ({self.num_tiles} tiles, "
                              f"{self.world_size} ranks)")
-        seed = None if seed is None else int(seed) * 1000003 + self.rank
+        seed = rank_seed(seed, self.rank)
         self.sampler = SMCsampler.from_tiles(
             local.reshape(1, -1, tile_dim, tile_dim), Prior, ImageModel, MutationKernel,
             num_catalogs, ess_threshold_prop, resample_method, flux_detection_threshold,
@@ -121,11 +126,16 @@ def gather_tile_results(local: dict, num_tiles: int, tiles_per_side, rank: int,
     sizes = [shard_tiles(num_tiles, world_size, r) for r in range(world_size)]
     counts = [b - a for a, b in sizes]
     tmax = max(counts)
+    # gloo gathers host tensors: device results are staged through the host
+    # (RCCL gathers device tensors directly, over xGMI)
+    host = dist.get_backend(group) == "gloo"
     out = {}
     for k in sorted(local):
         v = local[k]
         dtype = v.dtype
         flat = v.reshape(v.shape[0], -1).to(torch.float32)
+        if host:
+            flat = flat.cpu()
         pad = torch.zeros(tmax, flat.shape[1], dtype=torch.float32, device=flat.device)
         pad[: flat.shape[0]] = flat
         bufs = [torch.empty_like(pad) for _ in range(world_size)]
@@ -154,7 +164,7 @@ class ShardedBatchSMC:
         if self.stop <= self.start:
             raise ValueError(f"rank {self.rank} has no images ({self.num_images} images, "
                              f"{self.world_size} ranks)")
-        seed = None if seed is None else int(seed) * 1000003 + self.rank
+        seed = rank_seed(seed, self.rank)
         self.batch = BatchSMC(images[self.start:self.stop], Prior, ImageModel, MutationKernel,
                               num_catalogs, ess_threshold_prop, resample_method,
                               flux_detection_threshold, max_smc_iters, seed=seed, device=device,
@@ -186,7 +196,7 @@ class ShardedMCMC:
         if self.stop <= self.start:
             raise ValueError(f"rank {self.rank} has no images ({self.num_images} images, "
                              f"{self.world_size} ranks)")
-        seed = None if seed is None else int(seed) * 1000003 + self.rank
+        seed = rank_seed(seed, self.rank)
         b = self.stop - self.start
         H = images.shape[-1]
         tiles = images[self.start:self.stop].reshape(1, b, H, H)

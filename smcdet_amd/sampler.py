@@ -96,6 +96,9 @@ class SMCsampler(object):
         self._rate_age = 0
         self._fresh_loglik = None   # loglik of the current state, if already known
         self._pending_idx = None    # resampling indices computed by the fused tile launch
+        # optional callback(sampler) after every SMC iteration (e.g. to take a
+        # state_dict() checkpoint); runs the loop without speculation
+        self.on_iteration = None
 
     @classmethod
     def from_tiles(cls, tiles, *args, **kwargs):
@@ -345,6 +348,32 @@ class SMCsampler(object):
                         f"{round(acc.max().item(), 2)}]")
             print(msg)
 
+    def _progress_capture(self, stream):
+        """(event, pinned host copy) of this iteration's progress values
+        [tau min, tau max, acc min, acc max], or None when it prints nothing."""
+        if self.iter % self.print_every != 0:
+            return None
+        acc = getattr(self, "mutation_acc_rates", None)
+        t = self.temperature
+        vals = [t.min(), t.max()] + ([acc.min(), acc.max()] if acc is not None else [])
+        host = torch.empty(len(vals), dtype=torch.float32, pin_memory=True)
+        host.copy_(torch.stack(vals), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        return ev, host
+
+    def _progress_emit(self, line):
+        if line is None:
+            return
+        ev, host = line
+        ev.synchronize()
+        v = host.tolist()
+        msg = (f"iteration {self.iter}: "
+               f"temperature in [{round(v[0], 2)}, {round(v[1], 2)}]")
+        if len(v) == 4:
+            msg += f", acceptance rate in [{round(v[2], 2)}, {round(v[3], 2)}]"
+        print(msg)
+
     # ------------------------------------------------------- speculative loop
     _SNAPSHOT = ("locs", "fluxes", "counts", "mutation_acc_rates", "_fresh_loglik", "loglik",
                  "weights", "weights_log_unnorm", "ess", "temperature_prev", "_pending_idx",
@@ -358,7 +387,8 @@ class SMCsampler(object):
         hooks = ("_keep_going", "_temper_reweight", "mutate")
         return (all(h not in self.__dict__ and getattr(type(self), h) is getattr(SMCsampler, h)
                     for h in hooks)
-                and hasattr(self.MutationKernel, "_entry"))
+                and hasattr(self.MutationKernel, "_entry")
+                and getattr(self, "on_iteration", None) is None)
 
     def _run_speculative(self):
         """sampler.py:230-237 without a host round trip per iteration: the
@@ -395,7 +425,11 @@ class SMCsampler(object):
                 snap = {k: getattr(self, k, None) for k in self._SNAPSHOT}
                 rng_off = self.rng.offset
                 self.iter += 1
-                self._print_progress()
+                # the progress line of this iteration is printed only once the
+                # previous iteration's count shows that it runs (the reference
+                # prints it after its loop check); its values are captured now,
+                # asynchronously, before the kernels update them in place
+                line = self._progress_capture(main)
                 self._go = live_prev[2:3]
                 self._live_host = pinned.dev(1 - slot)
                 idx, self._pending_idx = self._pending_idx, None
@@ -411,6 +445,7 @@ class SMCsampler(object):
                         setattr(self, k, v)
                     self.rng.offset = rng_off
                     break
+                self._progress_emit(line)
                 live_prev, ev_prev, slot = self._live, ev, 1 - slot
         finally:
             self._go = self._live_host = None
@@ -429,22 +464,38 @@ class SMCsampler(object):
         self.iter = 0
         print("starting...")
         self.initialize()
-        if self.fused and self._can_speculate():
+        if self.fused:
             self._temper_reweight(with_resample=True)
+        else:
+            if self.stopping != "lockstep":
+                raise NotImplementedError("independent stopping runs on the fused schedule")
+            self.temper()
+            self.update_weights()
+        self._loop()
+        self._finish()
+
+    def resume(self):
+        """Continues a run from a state restored by load_state_dict() (a
+        state_dict() taken between SMC iterations, e.g. by `on_iteration`):
+        the rest of the loop, the final resample and prune.  With the rate
+        images in the checkpoint the result equals the uninterrupted run's."""
+        print("resuming...")
+        self._loop()
+        self._finish()
+
+    def _loop(self):
+        if self.fused and self._can_speculate() and getattr(self, "_live_valid", False):
             self._run_speculative()
         elif self.fused:
-            self._temper_reweight(with_resample=True)
             while self._keep_going() and self.iter <= self.max_smc_iters:
                 self.iter += 1
                 self._print_progress()
                 idx, self._pending_idx = self._pending_idx, None
                 self.mutate(ancestors=idx)
                 self._temper_reweight(with_resample=True)
+                if self.on_iteration is not None:
+                    self.on_iteration(self)
         else:
-            if self.stopping != "lockstep":
-                raise NotImplementedError("independent stopping runs on the fused schedule")
-            self.temper()
-            self.update_weights()
             while self._keep_going() and self.iter <= self.max_smc_iters:
                 self.iter += 1
                 self._print_progress()
@@ -452,6 +503,10 @@ class SMCsampler(object):
                 self.mutate()
                 self.temper()
                 self.update_weights()
+                if self.on_iteration is not None:
+                    self.on_iteration(self)
+
+    def _finish(self):
         self.resample()
         self.pruned_counts, self.pruned_locs, self.pruned_fluxes = self.prune(self.locs,
                                                                               self.fluxes)
@@ -483,25 +538,44 @@ class SMCsampler(object):
         print(f"number of unique catalogs = {self.fluxes[0, 0].sum(-1).unique(dim=0).shape[0]}")
 
     # ------------------------------------------------------------ checkpoint
-    def state_dict(self):
-        """Sampler state for checkpoint / resume (tensors stay on device)."""
-        keys = ("counts", "locs", "fluxes", "weights", "weights_log_unnorm", "ess",
-                "log_normalizing_constant", "temperature", "temperature_prev", "loglik")
-        st = {k: getattr(self, k) for k in keys if hasattr(self, k)}
-        st["iter"] = getattr(self, "iter", 0)
+    _CKPT_TENSORS = ("counts", "locs", "fluxes", "weights", "weights_log_unnorm", "ess",
+                     "log_normalizing_constant", "temperature", "temperature_prev", "loglik",
+                     "mutation_acc_rates", "iters_per_tile", "_pending_idx", "_fresh_loglik")
+
+    def state_dict(self, with_rate_images=True):
+        """Sampler state between SMC iterations, for checkpoint / resume
+        (copies of the device tensors: the kernels update some buffers in
+        place).  with_rate_images keeps the persisted per-particle rate images
+        ([numH,numW,N,H*W] float32), so that a resumed run continues exactly
+        as the uninterrupted one; without them the next sweep re-renders."""
+        st = {k: getattr(self, k).clone() for k in self._CKPT_TENSORS
+              if torch.is_tensor(getattr(self, k, None))}
+        st["iter"] = int(getattr(self, "iter", 0))
         st["rng"] = self.rng.state()
+        if with_rate_images and self._rate_valid and self._rate[self._rate_cur] is not None:
+            st["rate_image"] = self._rate[self._rate_cur].clone()
+            st["rate_age"] = int(self._rate_age)
         return st
 
     def load_state_dict(self, st):
-        for k, v in st.items():
-            if k == "rng":
-                self.rng.load_state(v)
-            elif k == "iter":
-                self.iter = v
-            else:
-                setattr(self, k, v.to(self.device) if torch.is_tensor(v) else v)
-        self._fresh_loglik = st.get("loglik")
-        self._pending_idx = None
+        """Restores a state_dict(); then resume() continues the run."""
+        for k in self._CKPT_TENSORS:
+            if k in st:
+                setattr(self, k, st[k].to(self.device).clone())
+            elif k in ("_pending_idx", "_fresh_loglik"):
+                setattr(self, k, None)
+        self.iter = int(st.get("iter", 0))
+        self.rng.load_state(st["rng"])
+        self.MutationKernel.rng = self.rng
+        self._live_valid = False
+        self._rate_valid = False
+        if "rate_image" in st:
+            r = st["rate_image"].to(self.device).clone()
+            self._rate = [r, torch.empty_like(r)]
+            self._rate_cur = 0
+            self._rate_age = int(st.get("rate_age", 0))
+            self._rate_valid = True
+        self.Prior.num = self.counts.shape[-1]
 
 
 class MHsampler(object):

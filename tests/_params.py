@@ -82,10 +82,17 @@ def mh_fixture_setup(name):
         return 8, o_m71_model(8), o_m71_prior(8, 3, 3), o_m71_mh(10)
     if name == "mh_basic_16x16":
         return 16, o_basic_model(16), o_basic_prior(16, 3, 3), o_basic_mh(20)
+    if name == "mh_m71_edge_8x8":
+        return 8, o_m71_model(8), o_m71_prior(8, 4, 4), o_m71_mh(30)
+    if name == "mh_m71_edge_32x32":
+        return 32, o_m71_model(32), o_m71_prior(32, 10, 10), o_m71_mh(24)
     raise KeyError(name)
 
 
-MH_FIXTURES = ["mh_m71_8x8", "mh_m71_32x32", "mh_m71_tiles", "mh_basic_16x16"]
+# the edge fixtures (make_golden.py gen_mh_edge) put location proposals exactly
+# on the prior box's upper edge: rejected, then the reference's NaN freeze
+MH_EDGE_FIXTURES = ["mh_m71_edge_8x8", "mh_m71_edge_32x32"]
+MH_FIXTURES = ["mh_m71_8x8", "mh_m71_32x32", "mh_m71_tiles", "mh_basic_16x16"] + MH_EDGE_FIXTURES
 
 
 def mala_fixture_setup(name):
@@ -156,6 +163,10 @@ def p_mh_fixture_setup(name, **kw):
         return 8, p_m71_model(8), p_m71_prior(8, 3, 3), p_m71_mh(10, **kw)
     if name == "mh_basic_16x16":
         return 16, p_basic_model(16), p_basic_prior(16, 3, 3), p_basic_mh(20, **kw)
+    if name == "mh_m71_edge_8x8":
+        return 8, p_m71_model(8), p_m71_prior(8, 4, 4), p_m71_mh(30, **kw)
+    if name == "mh_m71_edge_32x32":
+        return 32, p_m71_model(32), p_m71_prior(32, 10, 10), p_m71_mh(24, **kw)
     raise KeyError(name)
 
 

@@ -403,6 +403,171 @@ def gen_mh():
     save("mh_basic_16x16.npz", **d)
 
 
+def run_mh_edge_recorded(image, tile_dim, prior, model, mh, N, tau, seed, plan, u_hit=0.9999999):
+    """SingleComponentMH.run with sources placed just below the prior box's
+    upper edge (H + pad - 0.01) and draws injected so that chosen proposals
+    land exactly on it (distributions.py:44-48: p -> 1 - 1e-6, x rounds to
+    ub): Uniform.log_prob(high) = -inf (prior.py:73), the proposal is
+    rejected and the cached target becomes -inf * 0 = NaN (kernel.py:125), so
+    the particle rejects the rest of the sweep.  plan = [(particle, source,
+    coords, iteration)]: at `iteration` the particle's component is forced to
+    `source` and its location uniforms for `coords` (0 = h, 1 = w) to u_hit.
+    Records every draw actually used, every accept decision (prob <= alpha,
+    kernel.py:116) and the proposals."""
+    torch.manual_seed(seed)
+    s = sampler_for(image, tile_dim, prior, model, mh, N)
+    s.initialize()
+    hi = prior.loc_prior.high
+    for n, j, coords, _ in plan:
+        for c in coords:
+            s.locs[..., n, j, c] = float(hi[c]) - 0.01
+    nt = s.num_tiles_per_side
+    temperature = torch.full((nt, nt), float(tau))
+    proposals, accepts = [], []
+    orig = s.log_target
+
+    def log_target(data, counts, locs, fluxes, temperature):
+        v = orig(data, counts, locs, fluxes, temperature)
+        proposals.append((np32(locs), np32(fluxes), np32(v)))
+        return v
+
+    state = {"k": -1, "prob": None}
+    ms0, rand0 = torch.distributions.Multinomial.sample, torch.rand
+    usample0, le0 = torch.distributions.Uniform.sample, torch.Tensor.__le__
+
+    def ms(self_, sample_shape=torch.Size()):
+        out = ms0(self_, sample_shape)
+        state["k"] += 1
+        state["nrand"] = 0
+        S_ = out.shape[-1]
+        for n, j, _, k in plan:
+            if k == state["k"]:
+                out[..., n, :] = 0
+                out[..., n, j] = 1
+            elif state["k"] < k and bool((out[..., n, j] == 1).all()):
+                # keep the edge source where it was placed until its hit:
+                # farther from the edge, whether a draw rounds onto it
+                # depends on float32 rounding noise (a near-tie)
+                out[..., n, j] = 0
+                out[..., n, (j + 1) % S_] = 1
+        return out
+
+    def rand(*a, **kw):
+        out = rand0(*a, **kw)
+        if state["k"] >= 0:
+            state["nrand"] += 1
+            if state["nrand"] == 1:  # the location uniforms [nt,nt,N,S,2]
+                for n, j, coords, k in plan:
+                    if k == state["k"]:
+                        for c in coords:
+                            out[..., n, j, c] = u_hit
+        return out
+
+    def usample(self_, *a, **kw):
+        out = usample0(self_, *a, **kw)
+        state["prob"] = out
+        return out
+
+    def le(self_, other):
+        out = le0(self_, other)
+        if self_ is state["prob"]:
+            accepts.append(out.numpy().copy())
+        return out
+
+    locs0, fluxes0 = s.locs.clone(), s.fluxes.clone()
+    torch.distributions.Multinomial.sample = ms
+    torch.rand = rand
+    try:
+        with Recorder() as rec:
+            torch.distributions.Uniform.sample = usample
+            torch.Tensor.__le__ = le
+            try:
+                locs1, fluxes1, acc = mh.run(s.tiled_image, s.counts, s.locs, s.fluxes,
+                                             temperature, log_target)
+            finally:
+                torch.distributions.Uniform.sample = usample0
+                torch.Tensor.__le__ = le0
+    finally:
+        torch.distributions.Multinomial.sample = ms0
+        torch.rand = rand0
+    K = mh.num_iters
+    kinds = [k for k, _ in rec.draws]
+    assert kinds == ["mask", "rand", "rand", "rand"] * K, kinds[:8]
+    masks = np.stack([rec.draws[4 * i][1] for i in range(K)])
+    uloc = np.stack([rec.draws[4 * i + 1][1] for i in range(K)])
+    uflux = np.stack([rec.draws[4 * i + 2][1] for i in range(K)])
+    uacc = np.stack([rec.draws[4 * i + 3][1] for i in range(K)])
+    comp = masks.argmax(-1).astype(np.int32)
+    j = comp[..., None]
+    uloc_sel = np.take_along_axis(uloc, j[..., None].repeat(2, -1), axis=-2)[..., 0, :]
+    uflux_sel = np.take_along_axis(uflux, j, axis=-1)[..., 0]
+    prop_locs = np.stack([proposals[0][0]] + [proposals[i][0] for i in range(2, K + 1)])
+    accept = np.stack(accepts)
+    assert accept.shape == comp.shape, accept.shape
+    # the injected proposals did land on the edge
+    edge = np.zeros(comp.shape, bool)
+    hi32 = np.float32(hi.numpy())
+    for n, jj, coords, k in plan:
+        pl = prop_locs[k, :, :, n, jj]
+        edge[k, :, :, n] = np.any(pl[..., list(coords)] == hi32[list(coords)], -1)
+    assert edge.sum() == len(plan), (edge.sum(), len(plan))
+    return dict(image=np32(s.image), counts=np32(s.counts), locs0=np32(locs0),
+                fluxes0=np32(fluxes0), tau=np.float32(tau), comp=comp,
+                uloc=uloc_sel.astype(np.float32), uflux=uflux_sel.astype(np.float32),
+                uacc=uacc.astype(np.float32), locs1=np32(locs1), fluxes1=np32(fluxes1),
+                acc=np32(acc), accept=accept, edge_hit=edge, prop_locs=prop_locs,
+                init_logtarget=proposals[1][2],
+                locs_min=np32(mh.locs_min), locs_max=np32(mh.locs_max))
+
+
+def gen_mh_edge():
+    """Upper-edge proposals: M71 8x8 (S=4, N=32, K=30) and
+    the C2 geometry 32x32 (S=10, N=16, K=24); h, w and both coordinates on the
+    edge, hits early, mid-sweep and at the last iteration, and control
+    particles without hits."""
+    res = m71_truth_image(8, 45)
+    plan = [(0, 0, (0,), 0), (1, 1, (0,), 3), (2, 2, (1,), 5), (3, 3, (1,), 11),
+            (4, 0, (0, 1), 7), (5, 1, (0, 1), 29), (6, 2, (0,), 17), (7, 3, (1,), 22),
+            (8, 0, (1,), 1), (9, 2, (0,), 28)]
+    mh = SingleComponentMH(30, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    d = run_mh_edge_recorded(res[-1][0], 8, m71_prior(8, 4, 4), m71_model(8), mh, 32, 0.5,
+                             145, plan)
+    save("mh_m71_edge_8x8.npz", **d)
+    res = m71_truth_image(32, 46, counts_rate=0.003125, max_sources=10)
+    plan = [(0, 0, (0,), 0), (1, 4, (1,), 4), (2, 9, (0, 1), 9), (3, 5, (0,), 15),
+            (4, 7, (1,), 23), (5, 2, (0,), 12)]
+    # At 32x32 the reference's float32 log targets (1,024-pixel sums of terms
+    # ~10) carry ~1e-2 nats of rounding, which decides near-tie MH decisions;
+    # the kernels are exact to ~1e-6.  Take the first seed whose every decision
+    # the float64 oracle reproduces with a margin >= 5e-3 nats.
+    for seed in range(146, 200):
+        mh = SingleComponentMH(24, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+        d = run_mh_edge_recorded(res[-1][0], 32, m71_prior(32, 10, 10), m71_model(32), mh, 16,
+                                 0.2, seed, plan)
+        if _decisions_pinned(d, "mh_m71_edge_32x32", 5e-3):
+            break
+    save("mh_m71_edge_32x32.npz", **d)
+
+
+def _decisions_pinned(d, name, min_margin):
+    """True if the float64 oracle (oracle/smc_oracle.py) reproduces every
+    recorded decision of fixture d with |log U - log alpha| >= min_margin."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import smc_oracle as O
+    from tests._params import mh_fixture_setup, tiles_of
+    td, model, prior, mh = mh_fixture_setup(name)
+    t = tiles_of(d["image"], td)
+    tau = np.full(t.shape[:2], float(d["tau"]))
+    _, _, _, loga, acc = O.mh_sweep(t, d["counts"], d["locs0"], d["fluxes0"], tau, prior, model,
+                                    mh, d["comp"], d["uloc"], d["uflux"], d["uacc"], trace=True)
+    with np.errstate(all="ignore"):
+        m = np.abs(np.log(d["uacc"].astype(np.float64)) - np.minimum(loga, 0))
+    m = np.where(np.isfinite(m), m, np.inf)
+    ok = bool(np.array_equal(acc, d["accept"]) and m.min() >= min_margin)
+    print(name, "min margin %.2e" % m.min(), "decisions equal", np.array_equal(acc, d["accept"]))
+    return ok
+
+
 def run_mala_recorded(image, tile_dim, prior, model, mala, N, tau, seed):
     """Runs SingleComponentMALA.run (smcdet/kernel.py:133-275) once with
     recorded draws, gradients (torch.autograd.grad outputs) and proposals."""
@@ -673,11 +838,12 @@ def gen_smc_replay():
 
 
 # ----------------------------------------------------------------------------
-def gen_stats(which, seeds):
+def gen_stats(which, seeds, part=None):
     """Statistical targets: reference SMCsampler.run() over many seeds."""
     import contextlib
     import io
-    torch.set_num_threads(8)
+    torch.set_num_threads(int(os.environ.get("GOLDEN_THREADS", "8")))
+    max_iters = 100
     if which == "basic":
         res = basic_truth_image(16, 1)
         img = res[-1][0]
@@ -700,18 +866,37 @@ def gen_stats(which, seeds):
         mk = lambda: SingleComponentMALA(50, 0.1, 2.5, M71["flux_lower"],  # noqa: E731
                                          M71["flux_upper"])
         model, tile, N, method = m71_model(8), 8, 500, "systematic"
+    elif which == "c2_moderate":
+        # the headline geometry on a 32x32 tile of moderately bright stars
+        # (c2_moderate_truth_image): the reduced sampler (N=512, K=20) mixes on
+        # it, so log Z across seeds is tight enough to test at the 1% level
+        img = c2_moderate_truth_image()
+        pr = m71_prior(32, 10, 10, counts_rate=0.003125)
+        mk = lambda: SingleComponentMH(20, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])  # noqa
+        model, tile, N, method = m71_model(32), 32, 512, "systematic"
+        max_iters = 1000
+    elif which == "c2_reduced":
+        # the headline geometry (one 32x32 M71 tile, S=10,
+        # counts_rate 5/40^2 truth with <= 10 sources) at reduced N and K
+        res = m71_truth_image(32, 0, counts_rate=0.003125, max_sources=10)
+        img = res[-1][0]
+        pr = m71_prior(32, 10, 10, counts_rate=0.003125)
+        mk = lambda: SingleComponentMH(20, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])  # noqa
+        model, tile, N, method = m71_model(32), 32, 512, "systematic"
+        max_iters = 1000  # runs to temperature 1 take ~150-250 iterations here
     else:
         raise ValueError(which)
     rows = []
     for seed in seeds:
         torch.manual_seed(seed)
-        s = sampler_for(img, tile, pr, model, mk(), N, method=method)
-        esses = []
+        s = sampler_for(img, tile, pr, model, mk(), N, method=method, max_iters=max_iters)
+        esses, taus = [], []
         orig_uw = s.update_weights
 
-        def uw(s=s, esses=esses, orig_uw=orig_uw):
+        def uw(s=s, esses=esses, taus=taus, orig_uw=orig_uw):
             orig_uw()
             esses.append(float(s.ess.flatten()[0]))
+            taus.append(float(s.temperature.flatten()[0]))
 
         s.update_weights = uw
         t0 = time.perf_counter()
@@ -721,7 +906,7 @@ def gen_stats(which, seeds):
         pc = s.pruned_counts.flatten()
         hist = np.bincount(pc.numpy().astype(np.int64), minlength=pr.max_objects + 1)
         rows.append(dict(seed=seed, logZ=float(s.log_normalizing_constant.flatten()[0]),
-                         iters=int(s.iter), ess_trace=esses,
+                         iters=int(s.iter), ess_trace=esses, tau_trace=taus,
                          final_ess=float(s.ess.flatten()[0]),
                          pruned_hist=(hist / hist.sum()).tolist(),
                          mean_total_flux=float(s.posterior_mean_total_flux(s.fluxes).flatten()[0]),
@@ -730,12 +915,24 @@ def gen_stats(which, seeds):
                          runtime_s=dt))
         print(which, seed, rows[-1]["logZ"], rows[-1]["iters"], f"{dt:.1f}s", flush=True)
     cfg = dict(which=which, tile=tile, N=N, S=pr.max_objects, K=mk().num_iters, method=method,
-               rho=0.5, torch_threads=torch.get_num_threads(),
+               counts_rate=float(pr.counts_rate) if hasattr(pr, "counts_rate") else None,
+               rho=0.5, torch_threads=torch.get_num_threads(), max_smc_iters=max_iters,
                kernel="mala" if which.endswith("mala") else "mh")
-    path = os.path.join(HERE, f"stats_{which}.json")
+    path = os.path.join(HERE, f"stats_{which}.json" if part is None
+                        else f"stats_{which}.part{part}.json")
     with open(path, "w") as f:
         json.dump(dict(config=cfg, image=img.numpy().tolist(), runs=rows), f)
     print("wrote", path)
+
+
+def c2_moderate_truth_image():
+    """32x32 M71 image of four stars of 2-12 nmgy (peaks ~60-350 ADU over
+    the 104 ADU background) and one faint one, drawn with the reference's
+    M71ImageModel.sample."""
+    torch.manual_seed(72)
+    l = torch.tensor([[[[[7.3, 9.6], [21.8, 6.2], [15.1, 24.7], [26.4, 27.9], [4.2, 22.5]]]]])
+    f = torch.tensor([[[[12.0, 6.0, 4.0, 2.0, 0.8]]]])
+    return m71_model(32).sample(l, f)[0, 0, :, :, 0]
 
 
 def cssmc_truth_image():
@@ -795,20 +992,39 @@ if __name__ == "__main__":
         gen_prior()
         gen_distributions()
         gen_mh()
+        gen_mh_edge()
         gen_smc_steps()
         gen_smc_replay()
         gen_mala()
         gen_mcmc()
     elif what == "mala":
         gen_mala()
+    elif what == "mh-edge":
+        gen_mh_edge()
     elif what == "mcmc":
         gen_mcmc()
     elif what == "cssmc":
         n = int(sys.argv[2]) if len(sys.argv) > 2 else 16
         gen_cssmc(list(range(n)))
     elif what == "stats":
+        # stats <which> [n] [first]: seeds first..first+n-1; with `first` the
+        # rows go to stats_<which>.part<first>.json (parallel partial runs),
+        # merged by `stats-merge <which>`
         which = sys.argv[2]
         n = int(sys.argv[3]) if len(sys.argv) > 3 else 20
-        gen_stats(which, list(range(n)))
+        first = int(sys.argv[4]) if len(sys.argv) > 4 else None
+        gen_stats(which, list(range(first or 0, (first or 0) + n)), part=first)
+    elif what == "stats-merge":
+        import glob
+        which = sys.argv[2]
+        parts = sorted(glob.glob(os.path.join(HERE, f"stats_{which}.part*.json")))
+        docs = [json.load(open(p)) for p in parts]
+        runs = sorted((r for d in docs for r in d["runs"]), key=lambda r: r["seed"])
+        assert all(d["image"] == docs[0]["image"] for d in docs)
+        with open(os.path.join(HERE, f"stats_{which}.json"), "w") as f:
+            json.dump(dict(config=docs[0]["config"], image=docs[0]["image"], runs=runs), f)
+        for p in parts:
+            os.remove(p)
+        print("merged", len(runs), "runs from", len(parts), "parts")
     else:
         raise SystemExit(f"unknown target {what}")

@@ -29,7 +29,7 @@ def test_every_header_symbol_is_exported_and_bound():
 
 
 def test_version_and_abi():
-    assert _hip.lib().smcdet_abi_version() == 9
+    assert _hip.lib().smcdet_abi_version() == _hip.ABI_VERSION
     assert "gfx950" in _hip.version()
 
 
@@ -59,3 +59,16 @@ def test_product_refuses_host_tensors():
     import torch
     with pytest.raises(RuntimeError, match="HIP device"):
         _hip.dev_f32(torch.zeros(3), "x")
+
+
+def test_build_provenance():
+    """smcdet_version() carries the sha1 of the sources the library was built
+    from (Makefile SRC_HASH); it must equal the hash of the sources here, and
+    the Makefile must hash the same files in the same order as _hip.SOURCES."""
+    import re
+    mk = open(os.path.join(os.path.dirname(_hip._HERE), "Makefile")).read()
+    srcs = re.search(r"^SRCS := (.*)$", mk, re.M).group(1).replace("$(CSRC)", "smcdet_amd/csrc")
+    hdrs = re.search(r"^HDRS := (.*)$", mk, re.M).group(1).replace("$(CSRC)", "smcdet_amd/csrc")
+    listed = (srcs + " " + hdrs).split()
+    assert [os.path.relpath(p, os.path.dirname(_hip._HERE)) for p in _hip.SOURCES] == listed
+    assert _hip.built_hash() == _hip.source_hash()

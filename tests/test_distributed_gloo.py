@@ -133,3 +133,18 @@ def test_gather_and_lockstep_gloo(world):
     assert torch.equal(full["log_normalizing_constant"], -idx)
     assert full["pruned_counts"].dtype == torch.int64
     assert all(k[2] is True for k in keeps)  # rank 1 (and 2) still below 1
+
+
+def test_rank_seeds_distinct_and_rank0_identity():
+    """ADVICE r1: under torchrun every rank's torch.manual_seed is the same;
+    the kernels key draws by rank-local tile index, so the ranks' stream seeds
+    must differ.  Rank 0 keeps the base seed (a one-rank shard reproduces the
+    single-process sampler)."""
+    from smcdet_amd._rng import rank_seed
+    seeds = [rank_seed(12345, r) for r in range(64)]
+    assert seeds[0] == 12345 and len(set(seeds)) == 64
+    torch.manual_seed(0)
+    a = [rank_seed(None, r) for r in range(2)]
+    torch.manual_seed(0)
+    b = [rank_seed(None, r) for r in range(2)]
+    assert a[0] != a[1] and a == b  # each rank: same base from the same manual_seed

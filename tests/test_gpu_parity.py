@@ -12,7 +12,7 @@ import pytest
 import torch
 
 from oracle import smc_oracle as O
-from tests._params import (M71, MH_FIXTURES, golden, o_m71_model,
+from tests._params import (M71, MH_EDGE_FIXTURES, MH_FIXTURES, golden, o_m71_model,
                            p_basic_model, p_basic_prior, p_m71_model, p_m71_mh, p_m71_prior,
                            p_mh_fixture_setup, tiles_of)
 
@@ -385,3 +385,74 @@ def test_mh_persisted_rate_images_c2():
     fresh = model.rate(res[0][0], res[0][1])  # [1,1,H,W,N]
     fresh = fresh.permute(0, 1, 4, 2, 3).reshape(1, 1, Np, H * H)
     np.testing.assert_allclose(N(rates[1]), N(fresh), rtol=2e-6, atol=2e-4)
+
+
+@pytest.mark.parametrize("full", [False, True], ids=["incremental", "full"])
+@pytest.mark.parametrize("name", MH_EDGE_FIXTURES)
+def test_mh_edge_freeze_vs_reference(name, full):
+    """The reference's upper-edge fixtures (make_golden.py gen_mh_edge): the
+    particles whose proposal lands on the prior box's upper edge end the sweep
+    in the state they had before it (every later proposal rejected, the NaN
+    cache of kernel.py:125), bit for bit; the acceptance rate of the last
+    iteration counts them as rejections."""
+    d, l, f, acc, mh = _mh_replay(name, full)
+    hit = d["edge_hit"]
+    first = np.where(hit.any(0), hit.argmax(0), hit.shape[0])[0, 0]
+    frozen = np.nonzero(first < hit.shape[0])[0]
+    assert frozen.size >= 6
+    # state before the hit = the recorded proposal state at the hit iteration
+    # with the chosen source put back (prop_locs[k] = state_{k-1} but for j)
+    for n in frozen:
+        k, j = first[n], d["comp"][first[n], 0, 0, n]
+        before = d["prop_locs"][k, 0, 0, n].copy()
+        others = np.arange(before.shape[0]) != j
+        np.testing.assert_array_equal(N(l)[0, 0, n][others], before[others])
+        np.testing.assert_array_equal(N(l)[0, 0, n], d["locs1"][0, 0, n])
+    np.testing.assert_array_equal(N(acc), d["acc"])
+
+
+def test_rate_image_drift_long_run():
+    """Persisted rate images over a long run at temperature 1 (VERDICT r1
+    item 7): C2 geometry, N=1024, 48 sweeps of K=100, each starting from the
+    previous sweep's image and NEVER re-rendered (SMCsampler re-renders every
+    rate_refresh_every = 8 sweeps, so this bounds its drift from above).  After
+    every sweep the maintained image is compared with a fresh render of the
+    returned state and the returned log-likelihood with a fresh one.  Stated
+    bounds: |drift| <= 2e-6 * rate + 2e-4 ADU per pixel; log-likelihood within
+    rtol 2e-6 + atol 2e-2 nats (a few float32 ulps of the ~-5e3-nat sum)."""
+    from smcdet_amd._rng import PhiloxStream
+    torch.manual_seed(13)
+    H, S, Np, K, sweeps = 32, 10, 1024, 100, 48
+    model, prior = p_m71_model(H), p_m71_prior(H, S, S, counts_rate=0.003125)
+    truth = p_m71_prior(H, 0, 100, counts_rate=0.003125)
+    while True:
+        c, l, f = truth.sample(num_catalogs=1, device=DEV)
+        if 3 <= int(c.max()) <= S:
+            break
+    img = model.sample(l, f)[:, :, :, :, 0].contiguous()
+    counts, locs, fluxes = prior.sample(num_tiles_per_side=1, stratify_by_count=True,
+                                        num_catalogs_per_count=Np, device=DEV)
+    tau = torch.tensor([[1.0]], device=DEV)
+    rates = [torch.empty(1, 1, Np, H * H, device=DEV) for _ in range(2)]
+    mh = p_m71_mh(K)
+    mh.rng = PhiloxStream(9)
+    cur, worst_rate, worst_ll = None, 0.0, 0.0
+    moved = 0
+    for i in range(sweeps):
+        rin, rout = (None if i == 0 else rates[cur]), rates[0 if cur is None else 1 - cur]
+        l2, f2, acc = mh.run(img, counts, locs, fluxes, tau, prior=prior, image_model=model,
+                             rate_in=rin, rate_out=rout)
+        moved += int((l2 != locs).any(-1).any(-1).sum())
+        locs, fluxes = l2, f2
+        cur = 0 if cur is None else 1 - cur
+        fresh = model.rate(locs, fluxes).permute(0, 1, 4, 2, 3).reshape(1, 1, Np, H * H)
+        err = (rout - fresh).abs() - 2e-6 * fresh.abs()
+        worst_rate = max(worst_rate, float(err.max()))
+        ll = model.loglikelihood(img, locs, fluxes)
+        lerr = (mh.last_loglik - ll).abs() - 2e-6 * ll.abs()
+        worst_ll = max(worst_ll, float(lerr.max()))
+    print(f"rate-image drift over {sweeps} sweeps: {worst_rate:.3g} ADU beyond 2e-6 rel; "
+          f"loglik {worst_ll:.3g} nats beyond 2e-6 rel; {moved} particle-sweeps moved")
+    assert moved > sweeps * Np // 2  # the chains do move at temperature 1
+    assert worst_rate <= 2e-4, worst_rate
+    assert worst_ll <= 2e-2, worst_ll

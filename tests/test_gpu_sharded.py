@@ -1,0 +1,188 @@
+"""The tile-sharded multi-GPU path (smcdet_amd/distributed.py) on
+a device, and the C3 shape (a grid of 32x32 tiles through one SMCsampler).
+
+* A rank's shard keys its draws by rank-local tile index and rank 0 keeps the
+  base seed, so with independent stopping (each tile stops at temperature 1)
+  rank 0's shard reproduces the single-process run's first tiles bit for
+  bit, and rank r's shard reproduces a single-process run of its own tiles
+  with rank_seed(seed, r).
+* world_size 1 with a real gloo process group: gather_catalogs equals the
+  single-process sampler's attributes.
+* two processes (torchrun, gloo, both on cuda:0): the gathered catalogs equal
+  the two single-process runs of the shards' tiles.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from tests._params import M71, p_m71_mh, p_m71_model, p_m71_prior
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+H, N, K, S = 32, 256, 10, 10
+FIELDS = ("counts", "locs", "fluxes", "weights", "log_normalizing_constant", "ess",
+          "pruned_counts", "pruned_locs", "pruned_fluxes")
+
+
+def grid_image(tps, seed=5):
+    """tps x tps synthetic 32x32 M71 tiles (counts_rate 5/40^2, <= 10 sources)."""
+    from smcdet_amd.prior import M71Prior
+    model = p_m71_model(H)
+    truth = M71Prior(min_objects=0, max_objects=100, counts_rate=0.003125, image_height=H,
+                     image_width=H, flux_alpha=M71["flux_alpha"],
+                     flux_lower=M71["flux_detection_threshold"], flux_upper=M71["flux_upper"],
+                     pad=4)
+    torch.manual_seed(seed)
+    img = torch.empty(tps * H, tps * H, device="cuda")
+    for a in range(tps):
+        for b in range(tps):
+            while True:
+                c, l, f = truth.sample(num_catalogs=1, device="cuda")
+                if int(c.max()) <= S:
+                    break
+            img[a * H:(a + 1) * H, b * H:(b + 1) * H] = model.sample(l, f)[0, 0, :, :, 0]
+    return img
+
+
+def sampler(image_or_tiles, seed, stopping="independent", tiles=False):
+    from smcdet_amd.sampler import SMCsampler
+    args = (p_m71_prior(H, S, S, counts_rate=0.003125), p_m71_model(H), p_m71_mh(K), N, 0.5,
+            "systematic", M71["flux_detection_threshold"], 300)
+    kw = dict(print_every=10 ** 9, seed=seed, stopping=stopping)
+    if tiles:
+        return SMCsampler.from_tiles(image_or_tiles, *args, **kw)
+    return SMCsampler(image_or_tiles, H, *args, **kw)
+
+
+def shard(image, seed, rank, world, **kw):
+    from smcdet_amd.distributed import TileShardedSMC
+    return TileShardedSMC(image, H, p_m71_prior(H, S, S, counts_rate=0.003125), p_m71_model(H),
+                          p_m71_mh(K), N, 0.5, "systematic", M71["flux_detection_threshold"],
+                          300, seed=seed, rank=rank, world_size=world, **kw)
+
+
+def flat_tiles(s, f):
+    v = getattr(s, f)
+    return v.reshape(-1, *v.shape[2:]) if v.dim() >= 3 else v.reshape(-1)
+
+
+def test_rank_shards_reproduce_single_process_tiles():
+    from smcdet_amd._rng import rank_seed
+    img = grid_image(2)
+    single = sampler(img, 11)
+    single.run()
+    r0 = shard(img, 11, 0, 2, stopping="independent")
+    r0.run()
+    # rank 0 owns tiles 0, 1 (the top row): bit-equal to the single-process run
+    for f in FIELDS:
+        a, b = flat_tiles(r0.sampler, f), flat_tiles(single, f)[:2]
+        assert torch.equal(a, b), f
+    assert torch.equal(r0.sampler.iters_per_tile.flatten(), single.iters_per_tile.flatten()[:2])
+    # rank 1 (tiles 2, 3) runs with its own seed: equal to a single-process
+    # run of those tiles with that seed
+    r1 = shard(img, 11, 1, 2, stopping="independent")
+    r1.run()
+    tiles = img.unfold(0, H, H).unfold(1, H, H).reshape(1, 4, H, H)[:, 2:4].contiguous()
+    alone = sampler(tiles, rank_seed(11, 1), tiles=True)
+    alone.run()
+    for f in FIELDS:
+        assert torch.equal(flat_tiles(r1.sampler, f), flat_tiles(alone, f)), f
+    assert float(r1.sampler.temperature.min()) == 1.0
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_world1_gloo_gather_equals_single_process():
+    import torch.distributed as dist
+    img = grid_image(2, seed=6)
+    single = sampler(img, 21, stopping="lockstep")
+    single.run()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        from smcdet_amd.distributed import TileShardedSMC
+        sh = TileShardedSMC(img, H, p_m71_prior(H, S, S, counts_rate=0.003125), p_m71_model(H),
+                            p_m71_mh(K), N, 0.5, "systematic", M71["flux_detection_threshold"],
+                            300, seed=21, lockstep=True)
+        assert (sh.rank, sh.world_size) == (0, 1)
+        sh.run()
+        out = sh.gather_catalogs()
+    finally:
+        dist.destroy_process_group()
+    for f in FIELDS:
+        assert torch.equal(out[f].to(getattr(single, f).device), getattr(single, f)), f
+    assert int(out["iter"].flatten()[0]) == single.iter
+
+
+def test_two_process_gloo_gather_on_device(tmp_path):
+    """torchrun --nproc-per-node 2 (gloo; both ranks on cuda:0) runs
+    scripts/sharded_check.py: every rank samples its shard, rank 0 gathers
+    and saves the catalogs; they must equal the single-process runs of the
+    two shards' tiles."""
+    from smcdet_amd._rng import rank_seed
+    out = tmp_path / "gathered.pt"
+    env = dict(os.environ, SMCDET_SHARD_OUT=str(out), PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "scripts", "sharded_check.py")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    got = torch.load(out, weights_only=True)
+    img = grid_image(2, seed=7)
+    tiles = img.unfold(0, H, H).unfold(1, H, H).reshape(1, 4, H, H)
+    for rank, (a, b) in enumerate(((0, 2), (2, 4))):
+        alone = sampler(tiles[:, a:b].contiguous(), rank_seed(31, rank), tiles=True)
+        alone.run()
+        for f in FIELDS:
+            want = flat_tiles(alone, f).cpu()
+            have = got[f].reshape(4, *got[f].shape[2:])[a:b] if got[f].dim() > 2 else \
+                got[f].reshape(4)[a:b]
+            assert torch.equal(have.to(want.dtype), want), (rank, f)
+
+
+def test_c3_shape_grid_of_32x32_tiles():
+    """A 4x4 grid of 32x32 tiles (the C3 geometry at reduced N) through one
+    SMCsampler with the reference's lockstep stop: every tile reaches
+    temperature 1, log Z and ESS are finite, non-final ESS = rho*N, and each
+    tile's result is independent of its neighbours (equal to the same tile
+    sampled alone, independent stopping)."""
+    img = grid_image(4, seed=8)
+    s = sampler(img, 41, stopping="lockstep")
+    esses = []
+    orig = s._temper_reweight
+
+    def tr(with_resample, orig=orig):
+        orig(with_resample)
+        esses.append(s.ess.detach().clone())
+
+    s._temper_reweight = tr
+    s.run()
+    assert s.log_normalizing_constant.shape == (4, 4)
+    assert float(s.temperature.min()) == 1.0
+    assert torch.isfinite(s.log_normalizing_constant).all()
+    it = s.iters_per_tile.cpu().numpy()
+    assert (it > 0).all()
+    E = torch.stack(esses).cpu().numpy()  # [iters+1, 4, 4]
+    for t in range(16):
+        h, w = divmod(t, 4)
+        inner = E[: it[h, w], h, w]  # steps before the tile reached temperature 1
+        np.testing.assert_allclose(inner, 0.5 * N, rtol=0.01)
+    # independent stopping, same seed: the first tile's stream is the same
+    ind = sampler(img, 41, stopping="independent")
+    ind.run()
+    assert torch.equal(ind.iters_per_tile, s.iters_per_tile)
+    # log Z is fixed once a tile reaches temperature 1 (delta = 0), so the two
+    # modes agree on it even though lockstep keeps mutating finished tiles
+    assert torch.equal(ind.log_normalizing_constant, s.log_normalizing_constant)

@@ -31,6 +31,10 @@ def _load(which):
         return json.load(f)
 
 
+# the headline geometry (32x32, S=10, counts_rate 5/40^2) at N=512, K=20
+C2_TARGETS = ("c2_moderate", "c2_reduced")
+
+
 def _run(which, cfg, image, seed, fused=True, persist=True):
     from smcdet_amd.sampler import SMCsampler
     torch.manual_seed(seed)
@@ -41,23 +45,29 @@ def _run(which, cfg, image, seed, fused=True, persist=True):
         from smcdet_amd.kernel import SingleComponentMALA
         prior, model = p_m71_prior(H, S, S), p_m71_model(H)
         mh = SingleComponentMALA(cfg["K"], 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    elif which in C2_TARGETS:
+        prior, model = p_m71_prior(H, S, S, counts_rate=0.003125), p_m71_model(H)
+        mh = p_m71_mh(cfg["K"])
     else:
         prior, model, mh = p_m71_prior(H, S, S), p_m71_model(H), p_m71_mh(cfg["K"])
+    # SMCsampler's defaults: incremental MH, persisted rate images refreshed
+    # every 8 sweeps, lockstep stopping, speculative fused loop
     s = SMCsampler(image, H, prior, model, mh, N, cfg["rho"], cfg["method"],
-                   M71["flux_detection_threshold"], 100, print_every=10 ** 9, fused=fused,
-                   persist_rate_images=persist)
-    esses = []
+                   M71["flux_detection_threshold"], cfg.get("max_smc_iters", 100),
+                   print_every=10 ** 9, fused=fused, persist_rate_images=persist)
+    esses, taus = [], []
     orig = s._temper_reweight
 
     def tr(with_resample, orig=orig):
         orig(with_resample)
         esses.append(float(s.ess.flatten()[0]))
+        taus.append(float(s.temperature.flatten()[0]))
 
     s._temper_reweight = tr
     s.run()
     hist = np.bincount(s.pruned_counts.flatten().cpu().numpy(), minlength=S + 1)
     return dict(logZ=float(s.log_normalizing_constant.flatten()[0]), iters=s.iter,
-                ess_trace=esses, final_ess=float(s.ess.flatten()[0]),
+                ess_trace=esses, tau_trace=taus, final_ess=float(s.ess.flatten()[0]),
                 pruned_hist=hist / hist.sum(),
                 mean_total_flux=float(s.posterior_mean_total_flux(s.fluxes).flatten()[0]))
 
@@ -115,6 +125,66 @@ def test_statistical_parity_vs_reference(which):
     assert np.all(d <= 3 * se_bins + 0.01), (H.mean(0).round(3), H_ref.mean(0).round(3))
     if se_bins.max() < 0.01:
         assert 0.5 * d.sum() <= 0.05, (H.mean(0).round(3), H_ref.mean(0).round(3))
+
+
+@pytest.mark.parametrize("which", C2_TARGETS)
+def test_statistical_parity_c2_geometry(which):
+    """north_star's "log Z and ESS within 1%" at the headline geometry: one
+    32x32 M71 tile, S=10, counts_rate 5/40^2, with the reduced sampler
+    (N=512, K=20) of >= 24 reference seeds.
+      c2_moderate: four 2-12 nmgy stars; the sampler mixes, log Z has a
+        relative spread of ~1% across seeds: mean log Z within 1% and 3 SE,
+        ESS = rho*N at every non-final step, final ESS, iteration count and
+        total flux within 3 SE.
+      c2_reduced: a tile with a 10^4-ADU star, where N=512, K=20 does not mix:
+        the reference's own log Z spreads over -5.4e3 .. -3.3e5 (heavy tail),
+        so the test is distributional (medians of log Z and iteration counts
+        within a bootstrap 99.9% band, two-sample rank test p > 0.001)."""
+    from scipy.stats import mannwhitneyu
+    if not os.path.exists(os.path.join(GOLDEN, f"stats_{which}.json")):
+        pytest.skip(f"stats_{which}.json not generated")
+    ref = _load(which)
+    cfg = ref["config"]
+    image = torch.tensor(ref["image"], dtype=torch.float32, device="cuda")
+    n = 48
+    runs = [_run(which, cfg, image, 2000 + i) for i in range(n)]
+    rr = ref["runs"]
+    rho_n = cfg["rho"] * cfg["N"]
+    lz, lz_ref = np.array([r["logZ"] for r in runs]), np.array([r["logZ"] for r in rr])
+    it, it_ref = np.array([r["iters"] for r in runs]), np.array([r["iters"] for r in rr])
+    # ESS: every non-final step whose increment delta is >= 1e-3 sits on
+    # rho*N within 1%, in both samplers.  (Below that, brentq's xtol = 1e-6,
+    # which the device Brent iteration reproduces, is not small against delta:
+    # the first step's ESS is ~10, not 256 -- compared by mean instead.)
+    for r in list(runs) + list(rr):
+        e, t = np.array(r["ess_trace"][:-1]), np.array(r["tau_trace"][:-1])
+        delta = np.diff(np.concatenate([[0.0], t]))
+        np.testing.assert_allclose(e[delta >= 1e-3], rho_n, rtol=0.01)
+    e0, e0_ref = np.array([r["ess_trace"][0] for r in runs]), np.array(
+        [r["ess_trace"][0] for r in rr])
+    assert abs(e0.mean() - e0_ref.mean()) <= 3 * _se(e0, e0_ref), (e0.mean(), e0_ref.mean())
+    print(which, "log Z mean", lz.mean(), "ref", lz_ref.mean(), "median", np.median(lz),
+          "ref", np.median(lz_ref), "iters", it.mean(), "ref", it_ref.mean())
+    if which == "c2_moderate":
+        se = _se(lz, lz_ref)
+        diff = lz.mean() - lz_ref.mean()
+        assert abs(diff) <= 3 * se, (lz.mean(), lz_ref.mean(), se)
+        assert abs(diff) <= 0.01 * abs(lz_ref.mean()), (lz.mean(), lz_ref.mean())
+        fe = np.array([r["final_ess"] for r in runs])
+        fe_ref = np.array([r["final_ess"] for r in rr])
+        assert abs(fe.mean() - fe_ref.mean()) <= 3 * _se(fe, fe_ref), (fe.mean(), fe_ref.mean())
+        assert abs(it.mean() - it_ref.mean()) <= max(3 * _se(it, it_ref), 0.5)
+        fl = np.array([r["mean_total_flux"] for r in runs])
+        fl_ref = np.array([r["mean_total_flux"] for r in rr])
+        assert abs(fl.mean() - fl_ref.mean()) <= 3 * _se(fl, fl_ref), (fl.mean(), fl_ref.mean())
+    else:
+        rng = np.random.default_rng(0)
+        for a, b in ((lz, lz_ref), (it, it_ref)):
+            boot = np.array([np.median(rng.choice(b, b.size)) - np.median(rng.choice(a, a.size))
+                             for _ in range(4000)])
+            lo, hi = np.quantile(boot, [0.0005, 0.9995])
+            assert lo <= 0 <= hi, (np.median(a), np.median(b), lo, hi)
+            assert mannwhitneyu(a, b).pvalue > 1e-3
 
 
 def test_fused_run_equals_method_by_method_run():

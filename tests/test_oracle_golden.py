@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 from oracle import smc_oracle as O
-from tests._params import (M71, MALA_FIXTURES, MH_FIXTURES, golden, mala_fixture_setup,
+from tests._params import (M71, MALA_FIXTURES, MH_EDGE_FIXTURES, MH_FIXTURES, golden, mala_fixture_setup,
                            mh_fixture_setup, o_basic_model,
                            o_basic_prior, o_m71_mh, o_m71_model, o_m71_prior, tiles_of)
 
@@ -235,3 +235,29 @@ def test_c_oracle_mh_chain_replay(name, td, S):
     np.testing.assert_array_equal(acc, d["accept"])
     np.testing.assert_allclose(l, d["locs"], rtol=0, atol=1e-5)
     np.testing.assert_allclose(f, d["fluxes"], rtol=1e-6, atol=1e-4)
+
+
+@pytest.mark.parametrize("name", MH_EDGE_FIXTURES)
+def test_mh_edge_decisions_replay(name):
+    """Every accept decision of the reference's upper-edge fixture
+    (make_golden.py gen_mh_edge): the proposal that lands on the prior box's
+    upper edge is rejected and every later proposal of that particle too (the
+    NaN cache of kernel.py:125); the control particles keep moving."""
+    d = golden(name + ".npz")
+    td, model, prior, mh = mh_fixture_setup(name)
+    t = tiles_of(d["image"], td)
+    tau = np.full(t.shape[:2], float(d["tau"]))
+    _, _, _, _, acc_tr = O.mh_sweep(t, d["counts"], d["locs0"], d["fluxes0"], tau, prior, model,
+                                    mh, d["comp"], d["uloc"], d["uflux"], d["uacc"], trace=True)
+    np.testing.assert_array_equal(acc_tr, d["accept"])
+    hit = d["edge_hit"]
+    first = np.where(hit.any(0), hit.argmax(0), hit.shape[0])
+    frozen = np.arange(hit.shape[0])[:, None, None, None] >= first[None]
+    assert frozen.sum() > 0 and not d["accept"][frozen].any()
+    # without the freeze the edge proposal is still rejected, but the particle
+    # moves on: the final states of the frozen particles differ
+    l2, _, _, _, acc2 = O.mh_sweep(t, d["counts"], d["locs0"], d["fluxes0"], tau, prior, model,
+                                   mh, d["comp"], d["uloc"], d["uflux"], d["uacc"], trace=True,
+                                   edge_freeze=False)
+    assert not acc2[hit].any()
+    assert acc2[frozen].any()
