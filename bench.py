@@ -48,6 +48,13 @@ FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md (vector FP32, spec)
 B_ALG_PER_STEP = 248        # SURVEY §8d, S=10
 F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
 PMC_FILE = "pmc_mh_r01_s4.json"  # rocprofv3 FETCH_SIZE+WRITE_SIZE per MH launch (scripts/profile.sh)
+PMC_VALU_FILE = "pmc_valu_mh_r02.json"  # rocprofv3 SQ VALU counts per MH launch (scripts/profile.sh)
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions/s: 1 per SIMD per 4 cycles (measured 4.2)
+# the reference itself (torch CPU, smcdet/kernel.py) on the same workload, SURVEY §6 (build
+# container, 8 cores; the reference does not travel to the GPU box)
+REFERENCE_CPU = {"value": 8466.0, "unit": "particle-steps/sec", "cores": 8, "kind": "reference",
+                 "sample": "reference SingleComponentMH, 32x32, N=4096, S=10, 10 iterations at "
+                           "tau=0.3, torch 2.10 CPU float32 (SURVEY.md §6)"}
 
 
 def parse():
@@ -81,6 +88,8 @@ def parse():
     # skip the untimed complete run() (wall time to temperature 1), e.g. under
     # a profiler whose kernel averages should cover the timed steps only
     ap.add_argument("--no-full-run", action="store_true")
+    # skip the untimed comparison with the reference's recorded runs
+    ap.add_argument("--no-vs-ref", action="store_true")
     return ap.parse_args()
 
 
@@ -332,6 +341,99 @@ def bench_mcmc(args, dev, rank, world):
     }
 
 
+def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
+    """The binding resource (FP32 VALU issue).  reference_equivalent: SURVEY
+    §8d's FLOPs of the reference's full re-render per particle-step, which the
+    incremental kernel does not execute (~15x fewer).  executed: from the
+    kernel's own VALU instruction counts (rocprofv3 PMC pass, profiles/
+    PMC_VALU_FILE, same workload): wave-instructions issued per second against
+    the issue peak of 256 CUs x 4 SIMDs x one wave-instruction per 4 cycles at
+    2.4 GHz, and the FP32 FLOPs they execute (64 lanes; FMA 2, packed x2)."""
+    out = {"bound": "valu", "mh_particle_steps_per_s": mh_rate,
+           "reference_equivalent": {
+               "alg_flop_per_particle_step": f_alg,
+               "tflops": mh_rate * f_alg / 1e12, "peak_fp32_tflops": FP32_PEAK_TFLOPS,
+               "frac": mh_rate * f_alg / 1e12 / FP32_PEAK_TFLOPS}}
+    pmc = os.path.join(ROOT, "profiles", PMC_VALU_FILE)
+    if (os.path.exists(pmc) and args.workload == "c2" and args.kernel == "mh"
+            and not args.full_recompute):
+        try:
+            d = json.load(open(pmc))
+            per_step = d["per_particle_step"]
+            insts = per_step["SQ_INSTS_VALU"] * launch_steps     # wave-instructions per launch
+            flops = per_step["fp32_flop"] * launch_steps
+            t = mh_ms * 1e-3
+            out["executed"] = {
+                "valu_wave_insts_per_particle_step": per_step["SQ_INSTS_VALU"],
+                "fp32_flop_per_particle_step": per_step["fp32_flop"],
+                "valu_issue_rate": insts / t, "valu_issue_peak": VALU_ISSUE_PEAK,
+                "valu_issue_frac": insts / t / VALU_ISSUE_PEAK,
+                "tflops": flops / t / 1e12, "frac": flops / t / 1e12 / FP32_PEAK_TFLOPS,
+                "source": f"profiles/{PMC_VALU_FILE}"}
+        except Exception as e:  # never fail the bench line on it
+            out["executed"] = {"error": repr(e)}
+    return out
+
+
+def vs_reference(dev, which="c2_moderate", n_runs=48):
+    """North-star parity at the headline geometry, outside the timed region:
+    the reference's recorded runs (tests/golden/stats_<which>.json: one 32x32
+    M71 tile, S=10, N=512, K=20, systematic, >= 24 seeds) against n_runs runs
+    of this sampler on the same image -- one launch grid of n_runs independent
+    copies of the tile (independent stopping = one single-tile run per copy,
+    each with its own Philox streams).  Means and standard errors of log Z,
+    final ESS and SMC iterations."""
+    import numpy as np
+    from smcdet_amd.images import M71ImageModel
+    from smcdet_amd.kernel import SingleComponentMH
+    from smcdet_amd.prior import M71Prior
+    from smcdet_amd.sampler import SMCsampler
+    path = os.path.join(ROOT, "tests", "golden", f"stats_{which}.json")
+    if not os.path.exists(path):
+        return None
+    ref = json.load(open(path))
+    cfg, rr = ref["config"], ref["runs"]
+    p, H, S, N, K = M71, cfg["tile"], cfg["S"], cfg["N"], cfg["K"]
+    model = M71ImageModel(image_height=H, image_width=H, background=p["background"],
+                          psf_radius=p["psf_radius"], adu_per_nmgy=p["adu_per_nmgy"],
+                          psf_params=p["psf_params"], noise_additive=p["noise_additive"],
+                          noise_multiplicative=p["noise_multiplicative"])
+    prior = M71Prior(min_objects=S, max_objects=S, counts_rate=COUNTS_RATE_C2, image_height=H,
+                     image_width=H, flux_alpha=p["flux_alpha"], flux_lower=p["flux_lower"],
+                     flux_upper=p["flux_upper"], pad=4)
+    img = torch.tensor(ref["image"], dtype=torch.float32, device=dev)
+    tiles = img.reshape(1, 1, H, H).expand(1, n_runs, H, H).contiguous()
+    mh = SingleComponentMH(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"])
+    s = SMCsampler.from_tiles(tiles, prior, model, mh, N, cfg["rho"], cfg["method"],
+                              p["flux_detection_threshold"], cfg.get("max_smc_iters", 1000),
+                              print_every=10 ** 9, seed=4242, device=dev,
+                              stopping="independent")
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        s.run()
+    lz = s.log_normalizing_constant.flatten().double().cpu().numpy()
+    fe = s.ess.flatten().double().cpu().numpy()
+    it = s.iters_per_tile.flatten().double().cpu().numpy()
+
+    def ms(a):
+        a = np.asarray(a, dtype=np.float64)
+        return {"mean": float(a.mean()), "se": float(a.std(ddof=1) / np.sqrt(a.size)),
+                "median": float(np.median(a)), "n": int(a.size)}
+
+    out = {"target": f"tests/golden/stats_{which}.json ({len(rr)} reference runs; "
+                     f"{H}x{H}, S={S}, N={N}, K={K})"}
+    for key, ours, theirs in (("log_Z", lz, [r["logZ"] for r in rr]),
+                              ("final_ess", fe, [r["final_ess"] for r in rr]),
+                              ("iterations", it, [r["iters"] for r in rr])):
+        a, b = ms(ours), ms(theirs)
+        pooled = float(np.hypot(a["se"], b["se"]))
+        out[key] = {"ours": a, "reference": b,
+                    "rel_diff": (a["mean"] - b["mean"]) / abs(b["mean"]),
+                    "diff_in_pooled_se": (a["mean"] - b["mean"]) / pooled if pooled else None}
+    return out
+
+
 def _full_run(s2):
     """One complete run() on a fresh sampler: initialise, the SMC loop with its
     per-iteration stopping check, final resample, prune."""
@@ -448,19 +550,10 @@ def main():
                      "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": f"smcdet {args.kernel}_sweep_kernel", "kernel_ms": mh_ms,
                      "alg_bytes_per_particle_step": b_alg},
-        "compute": {"bound": "valu", "mh_particle_steps_per_s": mh_rate,
-                    "alg_flop_per_particle_step": f_alg,
-                    "achieved_alg_tflops": mh_rate * f_alg / 1e12,
-                    "peak_fp32_tflops": FP32_PEAK_TFLOPS,
-                    "frac": mh_rate * f_alg / 1e12 / FP32_PEAK_TFLOPS},
+        "compute": compute_block(args, mh_rate, f_alg, launch_steps, mh_ms),
         "smc": {"temperature_min": float(s.temperature.min()),
                 "acc_rate": float(s.mutation_acc_rates.mean()),
-                "ess_mean": float(s.ess.mean()),
-                # the reference tempers each step to ESS = rho*N (sampler.py:109-122, brentq
-                # on ESS(delta) - rho*N), so its per-step ESS is rho*N up to brentq's
-                # tolerance; tests/test_gpu_statistical.py checks the same against 20
-                # recorded reference runs
-                "ess_vs_ref": float(s.ess.mean()) / (0.5 * s.weights.shape[-1])},
+                "ess_mean": float(s.ess.mean())},
     }
     # SURVEY §8d also asks for the wall time to temperature 1: one complete
     # run() (initialise, SMC loop with its per-iteration stopping check, final
@@ -474,10 +567,16 @@ def main():
         out["smc"]["run_to_tau1"] = {"iterations": int(s2.iter), "wall_s": run_s,
                                      "ms_per_iteration": run_s / max(int(s2.iter), 1) * 1e3,
                                      "temperature_min": float(s2.temperature.min())}
+    if rank == 0 and args.workload == "c2" and args.kernel == "mh" and not args.no_vs_ref:
+        try:
+            out["smc"]["vs_reference"] = vs_reference(dev)
+        except Exception as e:  # report, never fail the bench line on it
+            out["smc"]["vs_reference"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
         try:
             out["cpu_baseline"] = cpu_baseline(args, cpu_tile.cpu().numpy(),
                                                args.cpu_baseline_seconds)
+            out["cpu_baseline"]["reference_measured"] = REFERENCE_CPU
         except Exception as e:  # report, never fail the bench line on it
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:

@@ -67,8 +67,9 @@ extern "C" {
 
 /* temper_reweight flags */
 /* independent stopping: a tile that entered at temperature 1 keeps it (delta
- * 0), gets uniform weights, an unchanged log Z and identity resampling
- * indices, so its final particles stay put while the other tiles run on.
+ * 0), gets uniform weights, an unchanged log Z and ESS (that of its last
+ * step) and identity resampling indices, so its final particles stay put
+ * while the other tiles run on.
  * Without it (the reference, sampler.py:230) such tiles are resampled and
  * mutated at temperature 1 until every tile has finished. */
 #define SMCDET_SMC_FREEZE_DONE 1u

@@ -11,10 +11,10 @@ stop_on_crash() {  # $1 = rc, $2 = step
   if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "stopping after $2"; exit "$1"; fi
 }
 if [ "${RUN_TESTS:-1}" = "1" ]; then
-  timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v -p no:cacheprovider \
+  timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -m gpu ${PYTEST_X--x} -v -p no:cacheprovider \
     --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
   stop_on_crash $? pytest
-  tail -4 gpurun_out/pytest_gpu.log
+  grep -E "^FAILED|passed|failed" gpurun_out/pytest_gpu.log | tail -15
   timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1
   stop_on_crash $? smoke
   tail -2 gpurun_out/smoke.log

@@ -356,7 +356,6 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   int bfl = 0;
   unsigned bmg = 1u;  // lane 3b+1: ceil(65536 / union-window width), for q / bw
   int bj = 0, batch_k0 = 0, batch_n = 0;
-  int k_loop = 0;  // the sweep's iteration counter (an edge hit ends it early)
   uint64_t dirty = 0;
   auto compute_batch = [&](int k0) {
     const int n_ = min(min(kBatch, kWave - (k0 & 63)), K - k0);
@@ -402,31 +401,13 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     const float hd0 = __shfl(bhd, max(lane - 2, 0), kWave);
     const float hd1 = __shfl(bhd, max(lane - 1, 0), kWave);
     // log alpha = (Hastings + prior term) + tau * dll, accepted iff it is >= log U
-    // (U <= min(1, exp(log alpha)) for U in [0, 1); nan rejects).  An edge hit
-    // carries log U = +inf: always rejected.
+    // (U <= min(1, exp(log alpha)) for U in [0, 1); nan rejects).
     bhs = (hd0 + hd1 + bhd) + bdp;  // -inf in lane 3b+2 iff entry b hits the edge
     blu = fast_log(__shfl(ru4, kl, kWave));
     bj = j;
     batch_k0 = k0;
     batch_n = n_;
     dirty = 0;
-    // The reference caches the rejected -inf log target as -inf * 0 = NaN
-    // (kernel.py:125), so every later proposal of this particle in the sweep
-    // is rejected too: the sweep ends at its first edge hit.  A hit at entry
-    // b > 0 ends the batch there, so that the batch is recomputed at the hit's
-    // iteration (a move accepted before it recomputes it anyway); a hit at
-    // entry 0 is the current iteration: it runs (rejected) and the loop ends.
-    // Only loop-carried values change, on this rare branch.
-    const uint64_t hb = __ballot(d == 2 && b == lb3 && bhs == -INFINITY);
-    if (hb) {
-      const int bh = (int)(__builtin_ctzll(hb) / 3);
-      if (bh > 0) {
-        batch_n = bh;
-      } else {
-        batch_k0 = K - 1;  // entry 0 at k = K - 1: the last iteration
-        k_loop = K - 1;
-      }
-    }
   };
 
   int accept = 0;
@@ -440,8 +421,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   // progress together and keep the SIMD saturated to the end.
   int prio_lvl = 0;
   __builtin_amdgcn_s_setprio(3);
-  for (k_loop = 0; k_loop < K; ++k_loop) {
-    const int k = k_loop;
+  for (int k = 0; k < K; ++k) {
     const int lvl = (k * 4) / K;
     if (lvl != prio_lvl) {
       prio_lvl = lvl;
@@ -452,7 +432,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     const int kl = k & 63;
     if (kl == 0) refill(k);
     if (k >= batch_k0 + batch_n) compute_batch(k);
-    int b = k_loop - batch_k0;  // (k_loop moves only when an edge hit ends the sweep)
+    int b = k - batch_k0;
     int j = readlane(bj, 3 * b);
     if ((dirty >> j) & 1ull) {
       compute_batch(k);
@@ -640,6 +620,16 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
 #ifdef SMCDET_TRACE
     tr_acc += accept;
 #endif
+    // An edge hit (log prior -inf) is rejected, and the reference caches the
+    // rejected -inf log target as -inf * 0 = NaN (kernel.py:125), so every
+    // later proposal of this particle in the sweep is rejected too: the state
+    // is final, the sweep ends.  (Measured: this per-iteration scalar test
+    // costs ~1% of the launch; once-per-batch forms that change loop-carried
+    // state cost 3-13% through register allocation)  Not
+    // reproduced: U = 0 exactly with an edge hit (probability 2^-24 per hit),
+    // where the reference accepts and its cached target becomes -inf, so it
+    // accepts every later proposal of the sweep; here the sweep ends.
+    if (P.hast == -INFINITY) break;
     if (accept) {
       if constexpr (FULL) {
         cur_ll = new_ll;

@@ -206,8 +206,11 @@ __global__ void prior_sample_kernel(DevPrior pr, int T, int N, int n_per_count, 
     uw = uloc[i * 2 + 1];
     uf = uflux[i];
   } else {
-    const uint64_t ctr = offset + (uint64_t)i;
-    U4 r = philox4x32((uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, kTagPriorLoc, k0, k1);
+    // keyed by particle (t*N + n) with the source in the counter, as the
+    // other kernels key theirs: a tile's draws do not depend on how many
+    // tiles the grid has (a rank's shard reproduces the single-process run)
+    const uint64_t ctr = offset + (uint64_t)s;
+    U4 r = philox4x32((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)tn, kTagPriorLoc, k0, k1);
     uh = u01(r.x);
     uw = u01(r.y);
     uf = u01(r.z);

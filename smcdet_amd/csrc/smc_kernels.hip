@@ -280,7 +280,8 @@ __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
         a.log_w[(size_t)t * N + i] = 0.0f;
         a.weights[(size_t)t * N + i] = 1.0f / (float)N;
       }
-      if (threadIdx.x == 0) a.ess[t] = (float)N;
+      // a.ess[t] keeps the ESS of the tile's last step, as a single-tile
+      // run of the reference reports it after its final resample
     }
     if (a.flags & kDoResample)
       for (int i = threadIdx.x; i < N; i += kTB) a.idx[(size_t)t * N + i] = i;

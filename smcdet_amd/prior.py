@@ -117,7 +117,7 @@ class PointProcessPrior(object):
         locs = torch.zeros(nH, nW, N, S, 2, device=device, dtype=torch.float32)
         fluxes = torch.zeros(nH, nW, N, S, device=device, dtype=torch.float32)
         rng = rng or PhiloxStream()
-        off = rng.take(nH * nW * N * S)
+        off = rng.take(S)  # counters per particle (the kernel keys draws by particle)
         cp = self._cprior()
         if uloc is not None:
             uloc = _hip.dev_f32(uloc.to(device), "uloc")

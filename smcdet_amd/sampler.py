@@ -280,7 +280,11 @@ class SMCsampler(object):
             prev_t = torch.empty_like(new_t)
         self.weights_log_unnorm = torch.empty_like(self.loglik)
         self.weights = torch.empty_like(self.loglik)
-        self.ess = torch.empty_like(new_t)
+        if self.stopping != "independent" or getattr(self, "ess", None) is None or \
+                self.ess.shape != new_t.shape:
+            self.ess = torch.empty_like(new_t)
+        # (independent stopping: updated in place -- a finished tile keeps the
+        # ESS of its last step)
         live = self._live_ws()
         idx = None
         off = 0

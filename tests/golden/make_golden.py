@@ -1018,8 +1018,11 @@ if __name__ == "__main__":
         import glob
         which = sys.argv[2]
         parts = sorted(glob.glob(os.path.join(HERE, f"stats_{which}.part*.json")))
-        docs = [json.load(open(p)) for p in parts]
-        runs = sorted((r for d in docs for r in d["runs"]), key=lambda r: r["seed"])
+        main = os.path.join(HERE, f"stats_{which}.json")
+        docs = ([json.load(open(main))] if os.path.exists(main) else []) + \
+            [json.load(open(p)) for p in parts]
+        runs = {r["seed"]: r for d in docs for r in d["runs"]}  # later parts win
+        runs = [runs[k] for k in sorted(runs)]
         assert all(d["image"] == docs[0]["image"] for d in docs)
         with open(os.path.join(HERE, f"stats_{which}.json"), "w") as f:
             json.dump(dict(config=docs[0]["config"], image=docs[0]["image"], runs=runs), f)
