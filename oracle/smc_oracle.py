@@ -515,7 +515,8 @@ class DrawStream:
     """Replays a recorded reference draw sequence (tests/golden/*replay*.npz)."""
 
     def __init__(self, npz):
-        keys = sorted(k for k in npz.files if k.startswith("draw_"))
+        names = npz.files if hasattr(npz, "files") else list(npz)
+        keys = sorted(k for k in names if k.startswith("draw_"))
         self.items = [(k.split("_", 2)[2], npz[k]) for k in keys]
         self.pos = 0
 
@@ -530,7 +531,9 @@ def smc_run_replay(image, tile_dim, prior, model, mh, num_catalogs, draws,
                    ess_threshold_prop=0.5, max_smc_iters=100,
                    flux_detection_threshold=0.0, dtype=np.float64):
     """SMCsampler.run (sampler.py:221-256) with systematic resampling, replaying
-    the recorded reference draws.  Returns a dict of the sampler's attributes."""
+    the recorded reference draws.  Returns a dict of the sampler's attributes
+    (plus min_margin: the smallest |log U - min(log alpha, 0)| of any MH
+    decision of the run, i.e. how close the run came to a near-tie)."""
     image = np.asarray(image, dtype=np.float32)
     nt = image.shape[0] // tile_dim
     tiled = image[: nt * tile_dim, : nt * tile_dim].reshape(nt, tile_dim, nt, tile_dim)
@@ -552,6 +555,7 @@ def smc_run_replay(image, tile_dim, prior, model, mh, num_catalogs, draws,
     W, ess, logZ = update_weights(ll, tau, tau_prev, logZ, N, dtype)
     it = 0
     acc = None
+    min_margin = np.inf
     trace = {"tau": [tau.copy()], "logZ": [logZ.copy()], "ess": [ess.copy()]}
     K = mh.num_iters
     while np.any(tau < 1) and it <= max_smc_iters:
@@ -570,9 +574,14 @@ def smc_run_replay(image, tile_dim, prior, model, mh, num_catalogs, draws,
             ul.append(np.take_along_axis(rl, j[..., None, None].repeat(2, -1), axis=-2)[..., 0, :])
             uf.append(np.take_along_axis(rf, j[..., None], axis=-1)[..., 0])
             ua.append(ra)
-        locs, fluxes, acc = mh_sweep(tiled, counts, locs, fluxes, tau, prior, model, mh,
-                                     np.stack(comp), np.stack(ul), np.stack(uf),
-                                     np.stack(ua), dtype)
+        locs, fluxes, acc, loga, _ = mh_sweep(tiled, counts, locs, fluxes, tau, prior, model,
+                                              mh, np.stack(comp), np.stack(ul), np.stack(uf),
+                                              np.stack(ua), dtype, trace=True)
+        with np.errstate(all="ignore"):
+            mg = np.abs(np.log(np.stack(ua).astype(np.float64)) - np.minimum(loga, 0))
+        mg = mg[np.isfinite(mg)]
+        if mg.size:
+            min_margin = min(min_margin, float(mg.min()))
         ll = loglikelihood(tiled, locs, fluxes, model, dtype)
         tau_prev = tau
         tau, _ = temper(ll, tau, rhoN, np.float32 if dtype == np.float32 else dtype)
@@ -587,7 +596,7 @@ def smc_run_replay(image, tile_dim, prior, model, mh, num_catalogs, draws,
     pc, pl, pf = prune(locs, fluxes, tile_dim, flux_detection_threshold)
     return dict(counts=counts, locs=locs, fluxes=fluxes, weights=W, ess=ess,
                 logZ=logZ, temperature=tau, iters=it, acc=acc, pruned_counts=pc,
-                pruned_locs=pl, pruned_fluxes=pf,
+                pruned_locs=pl, pruned_fluxes=pf, min_margin=min_margin,
                 trace={k: np.stack(v) for k, v in trace.items()})
 
 

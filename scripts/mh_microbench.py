@@ -30,24 +30,50 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--full", action="store_true", help="include the full-recompute variant")
     ap.add_argument("--only", default=None, help="run just this variant (for rocprofv3 --pmc)")
+    ap.add_argument("--tau", type=float, default=0.3)
+    # library-independent inputs (torch CPU generator + the c2_moderate fixture
+    # image), so that libraries whose prior/noise kernels draw different
+    # streams still time the MH sweep on identical states (scripts/ab_kernel.sh)
+    ap.add_argument("--state", choices=["torch", "device"], default="torch")
+    ap.add_argument("--warm", type=int, default=3, help="MH sweeps before timing (torch state)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     H, S, Np = a.tile, a.sources, a.particles
     nt = int(round(a.tiles ** 0.5))
     model, prior = p_m71_model(H), p_m71_prior(H, S, S, counts_rate=0.003125)
-    truth = p_m71_prior(H, 0, 100, counts_rate=0.003125)
-    img = torch.empty(nt, nt, H, H, device=dev)
-    for i in range(nt):
-        for j in range(nt):
-            while True:
-                c, l, f = truth.sample(num_catalogs=1, device=dev)
-                if int(c.max()) <= S:
-                    break
-            img[i, j] = model.sample(l, f)[0, 0, :, :, 0]
-    counts, locs, fluxes = prior.sample(num_tiles_per_side=nt, stratify_by_count=True,
-                                        num_catalogs_per_count=Np, device=dev)
-    tau = torch.full((nt, nt), 0.3, device=dev)
+    if a.state == "torch":
+        from tests._params import GOLDEN, M71
+        ref = json.load(open(os.path.join(GOLDEN, "stats_c2_moderate.json")))
+        assert H == 32, "--state torch uses the 32x32 fixture image"
+        img = torch.tensor(ref["image"], dtype=torch.float32).reshape(1, 1, H, H)
+        img = img.expand(nt, nt, H, H).contiguous().to(dev)
+        g = torch.Generator().manual_seed(1)
+        counts = torch.full((nt, nt, Np), float(S), device=dev)
+        locs = (torch.rand(nt, nt, Np, S, 2, generator=g) * (H + 8) - 4).to(dev)
+        al, lo, hi = M71["flux_alpha"], M71["flux_lower"], M71["flux_upper"]
+        u = torch.rand(nt, nt, Np, S, generator=g, dtype=torch.float64)
+        fl = ((hi ** al - u * hi ** al + u * lo ** al) / (lo ** al * hi ** al)) ** (-1 / al)
+        fluxes = fl.float().clamp(lo, hi).to(dev)
+    else:
+        truth = p_m71_prior(H, 0, 100, counts_rate=0.003125)
+        img = torch.empty(nt, nt, H, H, device=dev)
+        for i in range(nt):
+            for j in range(nt):
+                while True:
+                    c, l, f = truth.sample(num_catalogs=1, device=dev)
+                    if int(c.max()) <= S:
+                        break
+                img[i, j] = model.sample(l, f)[0, 0, :, :, 0]
+        counts, locs, fluxes = prior.sample(num_tiles_per_side=nt, stratify_by_count=True,
+                                            num_catalogs_per_count=Np, device=dev)
+    tau = torch.full((nt, nt), a.tau, device=dev)
+    if a.state == "torch" and a.warm:
+        from smcdet_amd._rng import PhiloxStream
+        mw = p_m71_mh(a.K)
+        mw.rng = PhiloxStream(123)
+        for _ in range(a.warm):
+            locs, fluxes, _ = mw.run(img, counts, locs, fluxes, tau, prior=prior, image_model=model)
     variants = {"incremental": (False, 0),
                 "no_likelihood": (False, _hip.SMCDET_MH_ABLATE_LIKELIHOOD if hasattr(
                     _hip, "SMCDET_MH_ABLATE_LIKELIHOOD") else 256),

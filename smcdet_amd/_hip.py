@@ -26,6 +26,33 @@ SMCDET_MH_SKIP_DONE = 4
 ABI_VERSION = 10
 SMCDET_SMC_FREEZE_DONE = 1
 
+# Shapes the kernels support (checked by the C ABI too; the samplers raise
+# ValueError at construction with these named, SMCsampler/MHsampler.__init__):
+MAX_TILE_PIXELS = 4096      # H*W: the tile image + one rate image per wave in LDS (64x64)
+MAX_SOURCES = 64            # S = Prior.max_objects: one source per lane
+MAX_PARTICLES = 16384       # N per tile: the tile kernel holds 32 log-likelihoods per thread
+MAX_TILES = 65535           # T: the MH grid's y dimension
+MAX_PSF_RADIUS = 64
+
+
+def check_limits(H, W, S, N=None, T=None, R=None, where="sampler"):
+    """ValueError naming the limit a configuration exceeds (the reference has
+    none: smcdet/sampler.py:25-31 tiles any image)."""
+    if H * W > MAX_TILE_PIXELS:
+        raise ValueError(f"{where}: a {H}x{W} tile has {H * W} pixels; the gfx950 kernels keep "
+                         f"the tile and one rate image per wavefront in LDS, at most "
+                         f"{MAX_TILE_PIXELS} pixels (64x64) -- use tile_dim <= 64")
+    if S > MAX_SOURCES:
+        raise ValueError(f"{where}: max_objects = {S} > {MAX_SOURCES} (one source per lane of a "
+                         "64-wide wavefront)")
+    if N is not None and N > MAX_PARTICLES:
+        raise ValueError(f"{where}: {N} particles per tile > {MAX_PARTICLES}")
+    if T is not None and T > MAX_TILES:
+        raise ValueError(f"{where}: {T} tiles > {MAX_TILES}")
+    if R is not None and not 0 <= R <= MAX_PSF_RADIUS:
+        raise ValueError(f"{where}: psf_radius {R} outside 0..{MAX_PSF_RADIUS}")
+
+
 c_f = ctypes.c_float
 c_i = ctypes.c_int32
 c_p = ctypes.c_void_p

@@ -40,6 +40,13 @@ class SMCsampler(object):
                  ess_threshold_prop, resample_method, flux_detection_threshold, max_smc_iters,
                  print_every=5, *, seed=None, device=None, fused=True, persist_rate_images=True,
                  rate_refresh_every=8, stopping="lockstep"):
+        # shapes the kernels cannot run raise here, naming the limit (before
+        # anything touches the device)
+        nt = (image.shape[0] * image.shape[1] if image.dim() == 4
+              else (image.shape[0] // tile_dim) ** 2)
+        _hip.check_limits(tile_dim, tile_dim, Prior.max_objects,
+                          getattr(Prior, "num_counts", 1) * num_catalogs, nt,
+                          getattr(ImageModel, "psf_radius", None), where="SMCsampler")
         if device is None:
             device = image.device if image.is_cuda else torch.device(
                 "cuda", torch.cuda.current_device())
@@ -606,6 +613,8 @@ class MHsampler(object):
                  flux_detection_threshold, num_samples_total, num_samples_burnin,
                  keep_every_k: int = 1, print_every: int = 1000, *, num_chains=1, seed=None,
                  device=None):
+        _hip.check_limits(tile_dim, tile_dim, Prior.max_objects,
+                          R=getattr(ImageModel, "psf_radius", None), where="MHsampler")
         if device is None:
             device = image.device if image.is_cuda else torch.device(
                 "cuda", torch.cuda.current_device())

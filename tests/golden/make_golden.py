@@ -806,6 +806,17 @@ def run_smc_recorded(image, tile_dim, prior, model, mh, N, method, seed, max_ite
     return s, trace, draws
 
 
+def _replay_margin(image, draws, S, K, N):
+    """Smallest MH decision margin of an oracle replay of recorded draws."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import smc_oracle as O
+    from tests._params import o_m71_mh, o_m71_model, o_m71_prior
+    d = {k: v for k, v in draws.items()}
+    r = O.smc_run_replay(image, 8, o_m71_prior(8, S, S), o_m71_model(8), o_m71_mh(K), N,
+                         O.DrawStream(d), flux_detection_threshold=M71["flux_detection_threshold"])
+    return r["min_margin"]
+
+
 def gen_smc_replay():
     # end-to-end replay: M71 8x8 tile, S=4, N=64, K=5, systematic
     res = m71_truth_image(8, 61)
@@ -821,11 +832,20 @@ def gen_smc_replay():
                trace_tau=np.stack(trace["tau"]), trace_logZ=np.stack(trace["logZ"]),
                trace_ess=np.stack(trace["ess"]), **draws)
     save("smc_replay_m71_8x8.npz", **out)
-    # 2x2 tiles of 8x8 (lockstep stop across tiles), S=3, N=32, K=4
+    # 2x2 tiles of 8x8 (lockstep stop across tiles), S=3, N=32, K=4.  The
+    # first seed from 162 whose every MH decision the float64 oracle makes
+    # with |log U - log alpha| >= 1e-4 nats (the reference's float32
+    # proposals and sums differ from exact arithmetic by ~1e-5 here), so the
+    # whole run is pinned exactly
     res = m71_truth_image(16, 62)
-    mh = SingleComponentMH(4, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
-    s, trace, draws = run_smc_recorded(res[-1][0], 8, m71_prior(8, 3, 3), m71_model(8), mh,
-                                       32, "systematic", 162, 100)
+    for seed in range(162, 262):
+        mh = SingleComponentMH(4, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+        s, trace, draws = run_smc_recorded(res[-1][0], 8, m71_prior(8, 3, 3), m71_model(8), mh,
+                                           32, "systematic", seed, 100)
+        margin = _replay_margin(np32(s.image), draws, 3, 4, 32)
+        print("smc_replay_m71_tiles seed", seed, "min margin %.2e" % margin, flush=True)
+        if margin >= 1e-4:
+            break
     out = dict(image=np32(s.image), tile_dim=np.int64(8), N=np.int64(32), K=np.int64(4),
                S=np.int64(3), iters=np.int64(s.iter), counts=np32(s.counts), locs=np32(s.locs),
                fluxes=np32(s.fluxes), weights=np32(s.weights), ess=np32(s.ess),
@@ -1001,6 +1021,8 @@ if __name__ == "__main__":
         gen_mala()
     elif what == "mh-edge":
         gen_mh_edge()
+    elif what == "smc-replay":
+        gen_smc_replay()
     elif what == "mcmc":
         gen_mcmc()
     elif what == "cssmc":

@@ -62,3 +62,37 @@ def test_mala_attributes_and_abi_fields():
     assert c.locs_stdev == pytest.approx(0.1) and c.fluxes_stdev == 2.5
     assert (c.locs_min_h, c.locs_max_w) == (-4.0, 12.0)
     assert k._entry == "smcdet_mala_sweep"
+
+
+def test_unsupported_shapes_fail_at_construction():
+    """tiles over 64x64 pixels, more than 64 sources or
+    more than 16,384 particles per tile raise ValueError naming the limit when
+    the sampler is built, before any kernel launch (the reference tiles any
+    image, smcdet/sampler.py:25-31)."""
+    from smcdet_amd.images import M71ImageModel
+    from smcdet_amd.kernel import SingleComponentMH
+    from smcdet_amd.prior import M71Prior
+    from smcdet_amd.sampler import MHsampler, SMCsampler
+
+    def make(H, S):
+        model = M71ImageModel(image_height=H, image_width=H, background=104.0, psf_radius=8,
+                              adu_per_nmgy=241.0, psf_params=[1.1, 2.1, 2.3, 5.2, 0.73, 0.51],
+                              noise_additive=1e-10, noise_multiplicative=1.94)
+        prior = M71Prior(min_objects=S, max_objects=S, counts_rate=0.003, image_height=H,
+                         image_width=H, flux_alpha=0.2, flux_lower=0.06, flux_upper=1800.0,
+                         pad=4)
+        return model, prior
+
+    mh = SingleComponentMH(10, 0.1, 2.5, 0.06, 1800.0)
+    img = torch.zeros(128, 128)
+    model, prior = make(128, 10)
+    with pytest.raises(ValueError, match="16384 pixels.*4096"):
+        SMCsampler(img, 128, prior, model, mh, 512, 0.5, "systematic", 0.25, 10)
+    with pytest.raises(ValueError, match="4096"):
+        MHsampler(img, 128, prior, model, 0.1, 2.5, 0.25, 100, 10)
+    model, prior = make(32, 80)
+    with pytest.raises(ValueError, match="max_objects = 80 > 64"):
+        SMCsampler(torch.zeros(32, 32), 32, prior, model, mh, 512, 0.5, "systematic", 0.25, 10)
+    model, prior = make(32, 10)
+    with pytest.raises(ValueError, match="20000 particles per tile > 16384"):
+        SMCsampler(torch.zeros(32, 32), 32, prior, model, mh, 20000, 0.5, "systematic", 0.25, 10)

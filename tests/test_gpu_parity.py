@@ -292,12 +292,13 @@ def _replay_smc(d, fused_mh_gather):
 @pytest.mark.parametrize("fused", [False, True], ids=["gather", "mh-gather"])
 @pytest.mark.parametrize("name", ["smc_replay_m71_8x8", "smc_replay_m71_tiles"])
 def test_smc_end_to_end_replay_vs_reference(name, fused):
-    """Whole SMC run driven by the reference's recorded draws.  The 8x8 run's
-    MH decisions all have margins |log U - log alpha| >= 2e-5 nats and are
-    reproduced exactly; the 2x2-tile run has decisions within 7e-5 nats of
-    the threshold, below the float32 noise of the proposal itself (torch's and
-    ocml's erfinv/erf differ by an ulp), so there a flipped near-tie may
-    perturb the temperature ladder at the 1e-4 level: checked loosely."""
+    """Whole SMC run driven by the reference's recorded draws.  Both fixtures'
+    MH decisions have margins |log U - log alpha| >= 2e-5 nats (8x8) and
+    >= 1e-4 nats (2x2 tiles of 8x8, lockstep stop; make_golden.py picks the
+    seed), above the float32 noise of the proposals themselves (torch's and
+    ocml's erfinv/erf differ by an ulp): the iteration count, the whole
+    temperature ladder, log Z, the final particles and the pruned counts are
+    reproduced exactly."""
     d = golden(name + ".npz")
     s, trace, pc = _replay_smc(d, fused)
     ref = d["trace_tau"]
@@ -306,19 +307,11 @@ def test_smc_end_to_end_replay_vs_reference(name, fused):
     msg = (f"iterations {s.iter} vs {int(d['iters'])}; first tau divergence at iteration "
            f"{bad[0] if len(bad) else None}")
     assert s.iter == int(d["iters"]), msg
-    exact = name == "smc_replay_m71_8x8"
-    np.testing.assert_allclose(trace, ref, rtol=0 if exact else 2e-3,
-                               atol=1e-5 if exact else 1e-5, err_msg=msg)
-    np.testing.assert_allclose(N(s.log_normalizing_constant), d["logZ"],
-                               rtol=1e-5 if exact else 2e-3)
-    np.testing.assert_allclose(N(s.ess), d["ess"], rtol=1e-4 if exact else 0.1)
-    if exact:
-        np.testing.assert_allclose(N(s.locs), d["locs"], rtol=0, atol=2e-5)
-        np.testing.assert_array_equal(N(pc), d["pruned_counts"])
-    else:
-        h1 = np.bincount(N(pc).ravel(), minlength=4) / pc.numel()
-        h2 = np.bincount(d["pruned_counts"].ravel(), minlength=4) / pc.numel()
-        assert 0.5 * np.abs(h1 - h2).sum() <= 0.15, (h1, h2)
+    np.testing.assert_allclose(trace, ref, rtol=0, atol=1e-5, err_msg=msg)
+    np.testing.assert_allclose(N(s.log_normalizing_constant), d["logZ"], rtol=1e-5)
+    np.testing.assert_allclose(N(s.ess), d["ess"], rtol=1e-4)
+    np.testing.assert_allclose(N(s.locs), d["locs"], rtol=0, atol=2e-5)
+    np.testing.assert_array_equal(N(pc), d["pruned_counts"])
 
 
 def test_mh_incremental_matches_full_recompute_c2():
