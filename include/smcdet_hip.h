@@ -240,7 +240,11 @@ int smcdet_mala_sweep(const smcdet_image_model_t* model,
  * mh->locs_stdev / fluxes_stdev / bounds as in smcdet_mh_sweep (the
  * reference takes the flux bounds from Prior.flux_lower/flux_upper).  Replay
  * buffers: comp [total-1,T,C], uloc [total-1,T,C,2], uflux / uacc
- * [total-1,T,C]. */
+ * [total-1,T,C].  frozen [T,C] int32 (nullable, zero before the first call):
+ * a chain whose location proposal lands on the prior box's upper edge
+ * rejects it and every later proposal of the run, as the reference's NaN
+ * cached target does (sampler.py:522-526); the flag carries that across
+ * chunked calls. */
 int smcdet_mh_chain(const smcdet_image_model_t* model,
                     const smcdet_prior_t* prior, const smcdet_mh_t* mh,
                     const float* tiled_image, int32_t T, int32_t C, int32_t S,
@@ -249,7 +253,8 @@ int smcdet_mh_chain(const smcdet_image_model_t* model,
                     int32_t keep_every_k, int32_t k_begin, int32_t k_end,
                     uint64_t seed, uint64_t offset,
                     const smcdet_mh_replay_t* replay, float* locs_out,
-                    float* fluxes_out, int32_t* accept_out, void* stream);
+                    float* fluxes_out, int32_t* accept_out, int32_t* frozen,
+                    void* stream);
 
 /* SMCsampler.temper (smcdet/sampler.py:93-125) on device: per tile, delta
  * solves exp(2 LSE(delta*l) - LSE(2 delta*l)) = ess_threshold on (0, 1-tau]

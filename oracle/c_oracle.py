@@ -80,8 +80,9 @@ def _pack(model, prior, mh):
 
 
 def mh_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mh, replay=None, seed=0,
-             threads=0):
-    """Runs the C sweep; returns (locs, fluxes, acc_rate[nH,nW])."""
+             threads=0, frozen_out=False):
+    """Runs the C sweep; returns (locs, fluxes, acc_rate[nH,nW]) (+ the
+    [nH,nW,N] mask of particles frozen by an upper-edge proposal)."""
     img = np.ascontiguousarray(tiled_image, dtype=np.float32)
     nH, nW, N, S, _ = np.shape(locs)
     T = nH * nW
@@ -101,7 +102,9 @@ def mh_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mh, replay=No
     lib().mh_oracle_sweep(ctypes.byref(m), ctypes.byref(p), ctypes.byref(h), P(img), P(c), P(l),
                           P(f), P(t), T, N, S, P(rc_), P(ru), P(rf), P(ra),
                           ctypes.c_uint64(seed), threads, P(acc))
-    return l, f, acc.reshape(nH, nW, N).mean(-1)
+    acc = acc.reshape(nH, nW, N)
+    rate = (acc == 1).mean(-1)
+    return (l, f, rate, acc == 2) if frozen_out else (l, f, rate)
 
 
 def mala_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mala, replay=None, seed=0,
@@ -154,12 +157,21 @@ def mh_chain(tiled_image, counts, init_locs, init_fluxes, prior, model, mh, tota
     if burnin == 0:
         kept_l.append(l[:, :, 0].copy())
         kept_f.append(f[:, :, 0].copy())
+    # an upper-edge proposal freezes the chain for the rest of the run
+    # (sampler.py:522-526 caches NaN as the current log target)
+    frozen = np.zeros((nH, nW), bool)
     for k in range(total - 1):
         rp = {"comp": replay["comp"][k][None, ..., None],
               "uloc": replay["uloc"][k][None, :, :, None],
               "uflux": replay["uflux"][k][None, ..., None],
               "uacc": replay["uacc"][k][None, ..., None]}
-        l, f, a = mh_sweep(tiled_image, c, l, f, 1.0, prior, model, m1, replay=rp, threads=1)
+        l2, f2, a, fz = mh_sweep(tiled_image, c, l, f, 1.0, prior, model, m1, replay=rp,
+                                 threads=1, frozen_out=True)
+        keep_old = frozen[..., None, None, None]
+        l = np.where(keep_old, l, l2)
+        f = np.where(frozen[..., None, None], f, f2)
+        a = np.where(frozen, 0.0, a)
+        frozen |= fz[..., 0]
         acc.append(a)
         m = k + 1
         if m >= burnin and (m - burnin) % keep == 0:

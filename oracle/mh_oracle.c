@@ -190,7 +190,8 @@ static double urand(uint64_t* s) { return (double)(splitmix(s) >> 40) * (1.0 / 1
  * [T,N,S,2] and fluxes [T,N,S] updated in place; tau [T].  Draws come from
  * the replay arrays (comp [K,T,N], uloc [K,T,N,2], uflux/uacc [K,T,N]) when
  * non-null, else from splitmix64 seeded by (seed, particle).  acc_last [T,N]
- * receives the accept flag of the last iteration.  Returns 0.
+ * receives the accept flag of the last iteration (2: the particle was frozen
+ * by an upper-edge proposal, a rejection).  Returns 0.
  */
 int mh_oracle_sweep(const om_model_t* m, const om_prior_t* pr, const om_mh_t* mh,
                     const float* image, const float* counts, float* locs, float* fluxes,
@@ -250,7 +251,7 @@ int mh_oracle_sweep(const om_model_t* m, const om_prior_t* pr, const om_mh_t* mh
          * cached target becomes -inf * 0 = NaN (kernel.py:125), which rejects
          * every remaining proposal of the sweep */
         if (nh >= pr->loc_high_h || nw >= pr->loc_high_w) {
-          acc = 0;
+          acc = 2; /* rejected, and frozen (reported as acc_last = 2) */
           break;
         }
         /* Hastings: the Normal log-densities cancel; log-mass-in-box terms remain */

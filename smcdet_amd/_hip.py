@@ -102,7 +102,7 @@ _SIGS = {
                            c_p, c_p, c_p, c_u64, c_u64, c_p, c_u32, c_p, c_p, c_p, c_p, c_p],
                           c_i),
     "smcdet_mh_chain": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_i, c_i, c_i, c_i,
-                         c_i, c_u64, c_u64, c_p, c_p, c_p, c_p, c_p], c_i),
+                         c_i, c_u64, c_u64, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
     "smcdet_temper": ([c_p, c_p, c_p, c_i, c_i, c_d, c_p], c_i),
     "smcdet_update_weights": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p], c_i),
     "smcdet_resample_index": ([c_p, c_i, c_i, c_i, c_u64, c_u64, c_p, c_p, c_p], c_i),

@@ -41,6 +41,7 @@ struct ChainArgs {
   float* locs_out;                   // [T,C,M,S,2] kept samples
   float* fluxes_out;                 // [T,C,M,S]
   int32_t* accept_out;               // [T,C,total-1] or null
+  int32_t* frozen;                   // [T,C] chain stopped by an edge hit (in/out) or null
   const int32_t* r_comp;             // replay [total-1,T,C] (or null)
   const float* r_uloc;
   const float* r_uflux;
@@ -162,7 +163,11 @@ __global__ __launch_bounds__(kChainBlock, 4) void mh_chain_kernel(ChainArgs a) {
     dirty = 0;
   };
 
-  for (int k = a.k_begin; k < a.k_end; ++k) {
+  // A chain whose proposal landed on the prior box's upper edge is frozen
+  // for the rest of the run (below); a later launch continues it frozen.
+  int k_end = (a.frozen && a.frozen[pid]) ? a.k_begin : a.k_end;
+  int k = a.k_begin;
+  for (; k < k_end; ++k) {
     const int kl = (k - a.k_begin) & 63;
     if (kl == 0) refill(k);
     if (k >= batch_k0 + batch_n) compute_batch(k);
@@ -265,6 +270,20 @@ __global__ __launch_bounds__(kChainBlock, 4) void mh_chain_kernel(ChainArgs a) {
     wave_sync();
     if (a.accept_out && lane == 0) a.accept_out[pid * (size_t)K + k] = accept;
     record(k + 1);
+    // An edge hit (Uniform.log_prob(high) = -inf, prior.py:73) is rejected,
+    // and the reference caches log_num_target * 0 = NaN as the current log
+    // target (sampler.py:522-526): every later proposal of the chain is
+    // rejected, for the rest of the run.
+    if (outside) {
+      ++k;
+      if (a.frozen && lane == 0) a.frozen[pid] = 1;
+      break;
+    }
+  }
+  // the frozen remainder: rejections, the same state recorded as the samples
+  for (; k < a.k_end; ++k) {
+    if (a.accept_out && lane == 0) a.accept_out[pid * (size_t)K + k] = 0;
+    record(k + 1);
   }
   if (lane < S) {
     a.locs_state[(pid * S + lane) * 2 + 0] = sh;
@@ -284,7 +303,8 @@ extern "C" int smcdet_mh_chain(const smcdet_image_model_t* model, const smcdet_p
                                int32_t num_samples_burnin, int32_t keep_every_k,
                                int32_t k_begin, int32_t k_end, uint64_t seed, uint64_t offset,
                                const smcdet_mh_replay_t* replay, float* locs_out,
-                               float* fluxes_out, int32_t* accept_out, void* stream) {
+                               float* fluxes_out, int32_t* accept_out, int32_t* frozen,
+                               void* stream) {
   int rc = validate_model(model);
   if (rc) return rc;
   rc = validate_prior(prior);
@@ -340,6 +360,7 @@ extern "C" int smcdet_mh_chain(const smcdet_image_model_t* model, const smcdet_p
   a.locs_out = locs_out;
   a.fluxes_out = fluxes_out;
   a.accept_out = accept_out;
+  a.frozen = frozen;
   if (replay) {
     a.r_comp = replay->comp;
     a.r_uloc = replay->uloc;

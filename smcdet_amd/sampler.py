@@ -722,6 +722,8 @@ class MHsampler(object):
         off = self.rng.take(max(K, 1))
         cm, cp, ch = self.ImageModel._cmodel(), self.Prior._cprior(), self._cmh()
         chunk = max(1, int(self.print_every))
+        # chains stopped by an upper-edge proposal (the reference's NaN cache)
+        frozen = torch.zeros(T * C, device=dev, dtype=torch.int32)
         k0 = 0
         while True:
             k1 = min(K, k0 + chunk)
@@ -729,7 +731,8 @@ class MHsampler(object):
                 _hip.ref(cm), _hip.ref(cp), _hip.ref(ch), _hip.ptr(self.tiled_image), T, C, S,
                 _hip.ptr(counts), _hip.ptr(ls), _hip.ptr(fs), total, burnin, keep, k0, k1,
                 self.rng.seed, off, _hip.ref(rp) if rp is not None else None, _hip.ptr(lo),
-                _hip.ptr(fo), _hip.ptr(acc), _hip.stream_of(ls)), "smcdet_mh_chain")
+                _hip.ptr(fo), _hip.ptr(acc), _hip.ptr(frozen), _hip.stream_of(ls)),
+                "smcdet_mh_chain")
             if k1 >= K:
                 break
             k0 = k1
@@ -738,6 +741,7 @@ class MHsampler(object):
                 print(f"iteration {k0}, acceptance rate in past {chunk} iters = {mean_acc:.2f}\n")
         del keepalive
         self.accept = acc[..., :K][:, :, 0] if C == 1 else acc[..., :K]
+        self.frozen = frozen.reshape(nH, nW, C)
         self.locs = lo.reshape(nH, nW, C * M, S, 2)
         self.fluxes = fo.reshape(nH, nW, C * M, S)
         self.counts = torch.full((nH, nW, C * M), float(S), device=dev)

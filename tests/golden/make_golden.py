@@ -662,23 +662,69 @@ def gen_mala():
     save("mala_basic_16x16.npz", **d)
 
 
-def run_mcmc_recorded(image, tile_dim, prior, model, total, burnin, keep, seed):
+def run_mcmc_recorded(image, tile_dim, prior, model, total, burnin, keep, seed, edge_plan=None,
+                      u_hit=0.9999999):
     """MHsampler (smcdet/sampler.py:301-493) with recorded draws: the initial
     prior draw, then per iteration the component mask, the location and flux
-    uniforms of the truncated normals and the accept uniform."""
+    uniforms of the truncated normals and the accept uniform.  edge_plan =
+    [(tile_h, tile_w, source, coords, iteration)]: that source starts 0.01
+    below the prior box's upper edge in `coords` and is kept still until
+    `iteration`, where it is chosen and its location uniforms are u_hit, so
+    the proposal lands exactly on the edge (log prior -inf: rejected, and the
+    chain's cached target becomes NaN, sampler.py:522-526)."""
     import contextlib
     import io
     torch.manual_seed(seed)
-    with Recorder() as rec:
-        s = MHsampler(image=image, tile_dim=tile_dim, Prior=prior, ImageModel=model,
-                      locs_stdev=0.1, fluxes_stdev=2.5,
-                      flux_detection_threshold=M71["flux_detection_threshold"],
-                      num_samples_total=total, num_samples_burnin=burnin, keep_every_k=keep,
-                      print_every=10 ** 9)
-        init_locs, init_fluxes = np32(s.locs[..., 0, :, :]), np32(s.fluxes[..., 0, :])
-        n_init = len(rec.draws)
-        with contextlib.redirect_stdout(io.StringIO()):
-            s.run()
+    ms0, rand0 = torch.distributions.Multinomial.sample, torch.rand
+    state = {"k": -1, "nrand": 0, "on": False}
+
+    def ms(self_, sample_shape=torch.Size()):
+        out = ms0(self_, sample_shape)
+        if state["on"]:
+            state["k"] += 1
+            state["nrand"] = 0
+            S_ = out.shape[-1]
+            for th, tw, j, _, k in edge_plan or ():
+                if state["k"] == k:
+                    out[th, tw, 0, :] = 0
+                    out[th, tw, 0, j] = 1
+                elif state["k"] < k and bool(out[th, tw, 0, j] == 1):
+                    out[th, tw, 0, j] = 0
+                    out[th, tw, 0, (j + 1) % S_] = 1
+        return out
+
+    def rand(*a, **kw):
+        out = rand0(*a, **kw)
+        if state["on"]:
+            state["nrand"] += 1
+            if state["nrand"] == 1:  # the location uniforms [nt,nt,1,S,2]
+                for th, tw, j, coords, k in edge_plan or ():
+                    if state["k"] == k:
+                        for c in coords:
+                            out[th, tw, 0, j, c] = u_hit
+        return out
+
+    torch.distributions.Multinomial.sample = ms
+    torch.rand = rand
+    try:
+        with Recorder() as rec:
+            s = MHsampler(image=image, tile_dim=tile_dim, Prior=prior, ImageModel=model,
+                          locs_stdev=0.1, fluxes_stdev=2.5,
+                          flux_detection_threshold=M71["flux_detection_threshold"],
+                          num_samples_total=total, num_samples_burnin=burnin,
+                          keep_every_k=keep, print_every=10 ** 9)
+            hi = prior.loc_prior.high
+            for th, tw, j, coords, _ in edge_plan or ():
+                for c in coords:
+                    s.locs[th, tw, 0, j, c] = float(hi[c]) - 0.01
+            init_locs, init_fluxes = np32(s.locs[..., 0, :, :]), np32(s.fluxes[..., 0, :])
+            n_init = len(rec.draws)
+            state["on"] = True
+            with contextlib.redirect_stdout(io.StringIO()):
+                s.run()
+    finally:
+        torch.distributions.Multinomial.sample = ms0
+        torch.rand = rand0
     draws = rec.draws[n_init:]
     K = total - 1
     kinds = [k for k, _ in draws]
@@ -699,6 +745,23 @@ def run_mcmc_recorded(image, tile_dim, prior, model, total, burnin, keep, seed):
                 accept=s.accept.numpy().astype(np.int32),
                 pruned_counts=s.pruned_counts.numpy().astype(np.int64),
                 pruned_locs=np32(s.pruned_locs), pruned_fluxes=np32(s.pruned_fluxes))
+
+
+def gen_mcmc_edge():
+    """MHsampler chains whose proposal lands on the prior box's upper edge
+    (2x2 tiles of 8x8, S=3, 240 samples, burn-in 40, every 2nd kept): tile
+    (0,0) at iteration 30 (h), tile (1,1) at iteration 120 (h and w); the other
+    two tiles run on.  The reference keeps those chains frozen for the rest of
+    the run (every later accept flag 0, every kept sample the same)."""
+    res = m71_truth_image(16, 63)
+    plan = [(0, 0, 1, (0,), 30), (1, 1, 2, (0, 1), 120)]
+    d = run_mcmc_recorded(res[-1][0], 8, m71_prior(8, 3, 3), m71_model(8), 240, 40, 2, 163,
+                          edge_plan=plan)
+    acc = d["accept"]
+    assert acc[0, 0, 30:].sum() == 0 and acc[1, 1, 120:].sum() == 0, "no freeze recorded"
+    assert acc[0, 1, 30:].sum() > 0 and acc[1, 0, 120:].sum() > 0
+    d["edge_plan"] = np.array([[th, tw, j, k] for th, tw, j, _, k in plan], np.int32)
+    save("mcmc_m71_edge_tiles.npz", **d)
 
 
 def gen_mcmc():
@@ -1017,6 +1080,7 @@ if __name__ == "__main__":
         gen_smc_replay()
         gen_mala()
         gen_mcmc()
+        gen_mcmc_edge()
     elif what == "mala":
         gen_mala()
     elif what == "mh-edge":
@@ -1025,6 +1089,8 @@ if __name__ == "__main__":
         gen_smc_replay()
     elif what == "mcmc":
         gen_mcmc()
+    elif what == "mcmc-edge":
+        gen_mcmc_edge()
     elif what == "cssmc":
         n = int(sys.argv[2]) if len(sys.argv) > 2 else 16
         gen_cssmc(list(range(n)))

@@ -172,3 +172,22 @@ def test_sharded_mcmc_single_rank_equals_mhsampler():
     assert tuple(res["locs"].shape) == (4, M, 3, 2)
     assert torch.equal(res["locs"], ref.locs[0]) and torch.equal(res["fluxes"], ref.fluxes[0])
     assert tuple(res["acc_rate"].shape) == (4,)
+
+
+@pytest.mark.parametrize("print_every", [10 ** 9, 37], ids=["one-launch", "chunked"])
+def test_mh_chain_edge_freeze_vs_reference(print_every):
+    """The reference's MHsampler chains whose proposal landed on the prior
+    box's upper edge (make_golden.py gen_mcmc_edge): rejected, then frozen for
+    the rest of the run -- every accept flag and kept sample equal to the
+    reference's, also when the run is chunked into launches of 37 iterations
+    (the freeze is carried in the chains' `frozen` flags)."""
+    d = golden("mcmc_m71_edge_tiles.npz")
+    s = _sampler(d["image"], 8, 3, d, print_every=print_every)
+    s.locs = torch.as_tensor(d["init_locs"][:, :, None], device=DEV)
+    s.fluxes = torch.as_tensor(d["init_fluxes"][:, :, None], device=DEV)
+    with __import__("contextlib").redirect_stdout(__import__("io").StringIO()):
+        s.run(replay=_replay(d))
+    np.testing.assert_array_equal(N(s.accept), d["accept"])
+    np.testing.assert_allclose(N(s.locs), d["locs"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(N(s.fluxes), d["fluxes"], rtol=2e-6, atol=1e-3)
+    np.testing.assert_array_equal(N(s.frozen)[..., 0], [[1, 0], [0, 1]])

@@ -261,3 +261,21 @@ def test_mh_edge_decisions_replay(name):
                                    edge_freeze=False)
     assert not acc2[hit].any()
     assert acc2[frozen].any()
+
+
+def test_c_oracle_mh_chain_edge_freeze():
+    """The C restatement replays the reference's frozen MHsampler chains
+    (make_golden.py gen_mcmc_edge): every accept flag and kept sample."""
+    from oracle import c_oracle
+    d = golden("mcmc_m71_edge_tiles.npz")
+    img = tiles_of(d["image"], 8)
+    replay = {k: d[k] for k in ("comp", "uloc", "uflux", "uacc")}
+    l, f, acc = c_oracle.mh_chain(img, np.full((2, 2), 3, np.float32), d["init_locs"],
+                                  d["init_fluxes"], o_m71_prior(8, 3, 3), o_m71_model(8),
+                                  o_m71_mh(1), int(d["total"]), int(d["burnin"]), int(d["keep"]),
+                                  replay)
+    np.testing.assert_array_equal(acc, d["accept"])
+    np.testing.assert_allclose(l, d["locs"], rtol=0, atol=1e-5)
+    plan = d["edge_plan"]
+    for th, tw, j, k in plan:
+        assert d["accept"][th, tw, k:].sum() == 0
