@@ -47,7 +47,7 @@ HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md (spec)
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md (vector FP32, spec)
 B_ALG_PER_STEP = 248        # SURVEY §8d, S=10
 F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
-PMC_FILE = "pmc_mh_r01_s4.json"  # rocprofv3 FETCH_SIZE+WRITE_SIZE per MH launch (scripts/profile.sh)
+PMC_FILE = "pmc_mh_r02.json"  # rocprofv3 FETCH_SIZE+WRITE_SIZE per MH launch (scripts/profile.sh)
 PMC_VALU_FILE = "pmc_valu_mh_r02.json"  # rocprofv3 SQ VALU counts per MH launch (scripts/profile.sh)
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions/s: 1 per SIMD per 4 cycles (measured 4.2)
 # the reference itself (torch CPU, smcdet/kernel.py) on the same workload, SURVEY §6 (build
@@ -361,11 +361,14 @@ def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
             d = json.load(open(pmc))
             per_step = d["per_particle_step"]
             insts = per_step["SQ_INSTS_VALU"] * launch_steps     # wave-instructions per launch
-            flops = per_step["fp32_flop"] * launch_steps
+            # SQ_INSTS_VALU_FLOPS_FP32(_TRANS) count FLOPs per wave-instruction
+            # (FMA 2, packed 2x): x 64 lanes
+            flops = 64 * per_step["fp32_flop"] * launch_steps
             t = mh_ms * 1e-3
             out["executed"] = {
                 "valu_wave_insts_per_particle_step": per_step["SQ_INSTS_VALU"],
-                "fp32_flop_per_particle_step": per_step["fp32_flop"],
+                "fp32_flop_per_particle_step": 64 * per_step["fp32_flop"],
+                "trans_wave_insts_per_particle_step": per_step.get("SQ_INSTS_VALU_TRANS_F32"),
                 "valu_issue_rate": insts / t, "valu_issue_peak": VALU_ISSUE_PEAK,
                 "valu_issue_frac": insts / t / VALU_ISSUE_PEAK,
                 "tflops": flops / t / 1e12, "frac": flops / t / 1e12 / FP32_PEAK_TFLOPS,

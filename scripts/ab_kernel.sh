@@ -14,9 +14,9 @@ for r in $(seq 1 $ROUNDS); do
     [ "$tag" != cur ] && lib=smcdet_amd/libsmcdet_hip_$tag.so
     out=gpurun_out/abk/${tag}_r$r.json
     SMCDET_ALLOW_STALE=1 SMCDET_HIP_LIB=$PWD/$lib timeout -k 10 180 python scripts/mh_microbench.py \
-      --only incremental --rounds 5 ${MB_ARGS:-} > $out 2> $out.err
+      --only ${MB_ONLY:-incremental} --rounds 5 ${MB_ARGS:-} > $out 2> $out.err
     rc=$?
     if [ $rc -ne 0 ]; then echo "$tag rc=$rc"; tail -5 $out.err; exit $rc; fi
-    python -c "import json; d=json.load(open('$out'))['variants']['incremental']; print('$tag', 'r$r', 'median_ms %.4f' % d['median_ms'], 'min_ms %.4f' % d['min_ms'])"
+    python -c "import json; d=json.load(open('$out'))['variants']['${MB_ONLY:-incremental}']; print('$tag', 'r$r', '${MB_ONLY:-incremental}', 'median_ms %.4f' % d['median_ms'], 'min_ms %.4f' % d['min_ms'])"
   done
 done
