@@ -262,12 +262,6 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     sw = a.locs_in[(src * S + lane) * 2 + 1];
     sfx = a.fluxes_in[src * S + lane];
   }
-  // per-source proposal caches at the current values
-  float ph_h, lZ_h, ph_w, lZ_w, ph_f, lZ_f;
-  tn_cache(sh, a.isl, a.lb_h, a.ub_h, ph_h, lZ_h);
-  tn_cache(sw, a.isl, a.lb_w, a.ub_w, ph_w, lZ_w);
-  tn_cache(sfx, a.isf, a.lb_f, a.ub_f, ph_f, lZ_f);
-  float lfx = fast_log(sfx);
   SMC_TRACE(trow, 2);
 
   double cur_ll = 0.0;  // tracked only in FULL mode (incremental mode works on deltas)
@@ -346,7 +340,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     }
   };
 
-  float bx = 0.f, bph = 0.f, blZ = 0.f, bhd = 0.f, blf = 0.f;
+  float bx = 0.f, bhd = 0.f;
   // per batch element b, precomputed in its lanes (amortised over the batch
   // instead of wave-uniform VALU work every iteration): bmu = current value
   // (lanes 3b+d); bfl = floor(current) | floor(proposed) << 16 (lanes 3b, 3b+1);
@@ -368,17 +362,17 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     const float u3 = __shfl(ru3, kl, kWave);
     const float u = d == 0 ? u1 : (d == 1 ? u2 : u3);
     const float m0 = __shfl(sh, j, kWave), m1 = __shfl(sw, j, kWave), m2 = __shfl(sfx, j, kWave);
-    const float q0 = __shfl(ph_h, j, kWave), q1 = __shfl(ph_w, j, kWave);
-    const float q2 = __shfl(ph_f, j, kWave);
-    const float z0 = __shfl(lZ_h, j, kWave), z1 = __shfl(lZ_w, j, kWave);
-    const float z2 = __shfl(lZ_f, j, kWave);
     const float mu = d == 0 ? m0 : (d == 1 ? m1 : m2);
-    const float c_ph = d == 0 ? q0 : (d == 1 ? q1 : q2);
-    const float c_lZ = d == 0 ? z0 : (d == 1 ? z1 : z2);
+    // the truncated normal's Phi(lb) and log-mass at the current value, in the
+    // lane that proposes the dimension (recomputed per batch rather than
+    // cached per source: no cache update on accept, fewer registers)
+    float c_ph, c_lZ;
+    tn_cache(mu, dm.isig, dm.lb, dm.ub, c_ph, c_lZ);
+    float n_ph, n_lZ, blf;
     if (ablate_prop)
-      propose_lane<true>(mu, c_ph, c_lZ, u, dm, bx, bph, blZ, bhd, blf);
+      propose_lane<true>(mu, c_ph, c_lZ, u, dm, bx, n_ph, n_lZ, bhd, blf);
     else
-      propose_lane<false>(mu, c_ph, c_lZ, u, dm, bx, bph, blZ, bhd, blf);
+      propose_lane<false>(mu, c_ph, c_lZ, u, dm, bx, n_ph, n_lZ, bhd, blf);
     bmu = mu;
     bfl = (int)(((unsigned)ifloor16(mu) & 0xffffu) | ((unsigned)ifloor16(bx) << 16));
     {  // union-window width of the column anchors (meaningful in lane 3b+1)
@@ -390,7 +384,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     // lane 3b+2 (flux): amplitudes, prior term (kernel.py:64-112 via
     // prior.py:220-226: the uniform location terms are constant in the box)
     // and the Hastings sum of the triple, in the per-iteration order
-    const float lf_cur = __shfl(lfx, j, kWave);
+    const float lf_cur = fast_log(mu);  // (lane 3b+2: mu = the current flux)
     bampo = m.g * mu * psf_scale<MODEL>(m);
     bampn = m.g * bx * psf_scale<MODEL>(m);
     bdp = ((float)j < count) ? -a.pr.ap1 * (blf - lf_cur) : 0.0f;
@@ -657,17 +651,10 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
         cur_ll += (double)dll;
         wave_sync();
       }
-      // source j takes the proposal and its proposal caches (v_writelane)
+      // source j takes the proposal (v_writelane)
       sh = writelane(P.hn, P.j, sh);
       sw = writelane(P.wn, P.j, sw);
       sfx = writelane(P.fn, P.j, sfx);
-      lfx = writelane(readlane(blf, 3 * b + 2), P.j, lfx);
-      ph_h = writelane(readlane(bph, 3 * b), P.j, ph_h);
-      lZ_h = writelane(readlane(blZ, 3 * b), P.j, lZ_h);
-      ph_w = writelane(readlane(bph, 3 * b + 1), P.j, ph_w);
-      lZ_w = writelane(readlane(blZ, 3 * b + 1), P.j, lZ_w);
-      ph_f = writelane(readlane(bph, 3 * b + 2), P.j, ph_f);
-      lZ_f = writelane(readlane(blZ, 3 * b + 2), P.j, lZ_f);
       dirty |= 1ull << P.j;
     }
   }
