@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 10
+#define SMCDET_ABI_VERSION 11
 
 /* status codes */
 #define SMCDET_OK 0
@@ -333,6 +333,71 @@ int smcdet_prune(const float* locs, const float* fluxes, int32_t T, int32_t N,
                  int32_t S, float tile_dim, float flux_threshold,
                  int64_t* counts_out, float* locs_out, float* fluxes_out,
                  void* stream);
+
+/* ---- tile aggregation (smcdet/aggregate.py:8-593, Aggregate) ------------- */
+#define SMCDET_AGG_MAX_SOURCES 256
+
+/* Aggregate.mutate (aggregate.py:176-187 with log_target :105-130): K =
+ * mh->num_iters single-component MH iterations on joint tiles of
+ * model->H x model->W pixels (T tiles, N particles, S source slots), under
+ *   log p(z) + (1 - tau) * [l_c1(z_1) + l_c2(z_2)] + tau * l_p(z),
+ * l_p the joint tile's image log-likelihood, l_c1 / l_c2 those of its two
+ * halves along `axis` (0: h, 1: w), each rendered from the sources whose axis
+ * coordinate is <= dim/2 (first half) or > dim/2 (second), the reference's
+ * unjoin (aggregate.py:265-324).  The moved component is drawn from
+ * 0..count-1 (slots past the count hold zero flux and never move); proposals,
+ * accept rule and the upper-edge freeze as smcdet_mh_sweep.  Reads particle
+ * ancestors[t,n] (identity when null) from *_in; counts_out nullable.
+ * loglik_parent / loglik_children [T,N] (nullable): l_p and l_c1 + l_c2 of the
+ * returned state, from a fresh render (num_iters = 0 evaluates the input
+ * state).  acc_rate [T] (nullable) = acceptance rate of the last iteration,
+ * with acc_count [2T] as in smcdet_mh_sweep.  Replay layout as
+ * smcdet_mh_replay_t (comp must be < count). */
+int smcdet_aggregate_sweep(const smcdet_image_model_t* model,
+                           const smcdet_prior_t* prior, const smcdet_mh_t* mh,
+                           int32_t axis, const float* tiled_image,
+                           const float* temperature, int32_t T, int32_t N,
+                           int32_t S, const int64_t* ancestors,
+                           const float* counts_in, const float* locs_in,
+                           const float* fluxes_in, float* counts_out,
+                           float* locs_out, float* fluxes_out, uint64_t seed,
+                           uint64_t offset, const smcdet_mh_replay_t* replay,
+                           float* loglik_parent, float* loglik_children,
+                           float* acc_rate, int32_t* acc_count, void* stream);
+
+/* Aggregate.temper (aggregate.py:140-174), per count group: the particles of
+ * each joint tile are sorted by count and split into G segments (count
+ * groups) given by seg_tile[g], seg_start[g] (first particle within the
+ * tile) and seg_len[g] (device int32 arrays).  With l = loglik_parent -
+ * loglik_children, delta[g] solves exp(2 LSE(delta*l) - LSE(2 delta*l)) =
+ * ess_threshold_prop * seg_len[g] on (0, 1 - tau] (brentq, xtol = rtol =
+ * 1e-6), or is 1 - tau when the ESS there is still above it. */
+int smcdet_aggregate_temper(const float* loglik_parent,
+                            const float* loglik_children,
+                            const float* temperature, int32_t T, int32_t N,
+                            int32_t G, const int32_t* seg_tile,
+                            const int32_t* seg_start, const int32_t* seg_len,
+                            double ess_threshold_prop, float* delta,
+                            void* stream);
+
+/* Aggregate.update_weights (aggregate.py:439-483) + resample_intracount
+ * (:485-521) per count group, after the caller has set temperature[t] to
+ * temperature_prev[t] + the minimum of the tile's delta[g] (aggregate.py:171-
+ * 174).  Per segment: log_weights_unnorm = (temperature - temperature_prev) *
+ * l (float32), weights_intracount = softmax within the segment,
+ * log_norm_const[g] += log mean exp(log w) (in place), ess[g] = 1 / sum w^2.
+ * idx [T,N] (nullable): tile-local multinomial resampling indices drawn within
+ * each segment from its weights (u [T,N] replays the uniforms). */
+int smcdet_aggregate_reweight(const float* loglik_parent,
+                              const float* loglik_children,
+                              const float* temperature,
+                              const float* temperature_prev, int32_t T,
+                              int32_t N, int32_t G, const int32_t* seg_tile,
+                              const int32_t* seg_start, const int32_t* seg_len,
+                              float* log_weights_unnorm,
+                              float* weights_intracount, float* log_norm_const,
+                              float* ess, uint64_t seed, uint64_t offset,
+                              const float* u, int64_t* idx, void* stream);
 
 #ifdef __cplusplus
 }

@@ -12,7 +12,7 @@ from . import _hip  # noqa: F401
 
 __version__ = "0.1.0"
 
-_DROP_IN = ("sampler", "kernel", "images", "prior", "distributions")
+_DROP_IN = ("sampler", "kernel", "images", "prior", "distributions", "aggregate")
 
 
 def install_as_smcdet():

@@ -23,7 +23,7 @@ SMCDET_RESAMPLE_SYSTEMATIC = 1
 SMCDET_MH_FULL_RECOMPUTE = 1
 SMCDET_MH_COMPONENT_BY_COUNT = 2
 SMCDET_MH_SKIP_DONE = 4
-ABI_VERSION = 10
+ABI_VERSION = 11
 SMCDET_SMC_FREEZE_DONE = 1
 
 # Shapes the kernels support (checked by the C ABI too; the samplers raise
@@ -33,6 +33,7 @@ MAX_SOURCES = 64            # S = Prior.max_objects: one source per lane
 MAX_PARTICLES = 16384       # N per tile: the tile kernel holds 32 log-likelihoods per thread
 MAX_TILES = 65535           # T: the MH grid's y dimension
 MAX_PSF_RADIUS = 64
+MAX_AGG_SOURCES = 256       # sources of an aggregated (joint) tile: catalog in LDS
 
 
 def check_limits(H, W, S, N=None, T=None, R=None, where="sampler"):
@@ -112,6 +113,12 @@ _SIGS = {
     "smcdet_count_posterior": ([c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_u64, c_u64, c_p, c_p,
                                 c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
     "smcdet_prune": ([c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p, c_p, c_p, c_p], c_i),
+    "smcdet_aggregate_sweep": ([c_p, c_p, c_p, c_i, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p,
+                                c_p, c_p, c_p, c_u64, c_u64, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
+    "smcdet_aggregate_temper": ([c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_d, c_p, c_p],
+                                c_i),
+    "smcdet_aggregate_reweight": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p,
+                                   c_p, c_p, c_u64, c_u64, c_p, c_p, c_p], c_i),
 }
 EXPORTS = tuple(_SIGS)
 
@@ -124,7 +131,7 @@ SOURCES = tuple(os.path.join(_REPO, p) for p in (
     "smcdet_amd/csrc/common.hip", "smcdet_amd/csrc/model_kernels.hip",
     "smcdet_amd/csrc/mh_kernel.hip", "smcdet_amd/csrc/mala_kernel.hip",
     "smcdet_amd/csrc/chain_kernel.hip", "smcdet_amd/csrc/smc_kernels.hip",
-    "smcdet_amd/csrc/device.h", "smcdet_amd/csrc/render.h", "smcdet_amd/csrc/mcmc.h",
+    "smcdet_amd/csrc/agg_kernel.hip", "smcdet_amd/csrc/device.h", "smcdet_amd/csrc/render.h", "smcdet_amd/csrc/mcmc.h",
     "include/smcdet_hip.h"))
 
 

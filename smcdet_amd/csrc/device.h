@@ -130,6 +130,9 @@ enum RngTag : uint32_t {
   kTagMALA1 = 0x4d4c0001u,
   kTagChain0 = 0x43480000u,
   kTagChain1 = 0x43480001u,
+  kTagAgg0 = 0x41470000u,
+  kTagAgg1 = 0x41470001u,
+  kTagAggResample = 0x41520000u,
 };
 
 // ---------------------------------------------------------------------------

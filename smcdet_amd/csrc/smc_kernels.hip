@@ -674,6 +674,171 @@ __global__ __launch_bounds__(256) void count_posterior_kernel(CountPostArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Tile aggregation (smcdet/aggregate.py:140-174 temper, :439-483
+// update_weights, :485-521 resample_intracount): the particles of a joint
+// tile are sorted by count, and each count group ("segment": tile, first
+// particle, length) is its own SMC population.  One 512-thread workgroup per
+// segment: pass A solves the segment's tempering increment with the same
+// Brent iteration as tile_kernel (ESS target ess_prop * group size); the
+// tile's increment is the minimum over its segments (a scatter-min by the
+// caller); pass B reweights each segment at the new temperature (softmax
+// within the group, log evidence of the group) and draws the intracount
+// multinomial resampling indices for the next iteration.  The
+// log-likelihood increment is loglik_parent - loglik_children (:539-541).
+// ---------------------------------------------------------------------------
+struct AggTileArgs {
+  int T, N, G;
+  double ess_prop;
+  const float* ll_parent;   // [T,N]
+  const float* ll_child;    // [T,N]
+  const int32_t* seg_tile;  // [G]
+  const int32_t* seg_start; // [G] first particle (within the tile)
+  const int32_t* seg_len;   // [G]
+  const float* temperature; // [T]
+  const float* temperature_prev; // [T]
+  float* delta;             // [G]
+  float* log_w;             // [T,N]
+  float* w_intra;           // [T,N]
+  float* lnc;               // [G] in/out
+  float* ess;               // [G]
+  uint32_t k0, k1;
+  uint64_t offset;
+  const float* u;           // [T,N] replayed uniforms or null
+  int64_t* idx;             // [T,N] or null (tile-local particle indices)
+};
+
+// the segment's (tile, first particle, length), clamped into [0,T) x [0,N)
+__device__ __forceinline__ void agg_segment(const AggTileArgs& a, int g, int& t, int& s0,
+                                            int& n) {
+  t = min(max(a.seg_tile[g], 0), a.T - 1);
+  s0 = min(max(a.seg_start[g], 0), a.N);
+  n = min(max(a.seg_len[g], 0), a.N - s0);
+}
+
+template <int PER>
+__global__ __launch_bounds__(kTB) void agg_temper_kernel(AggTileArgs a) {
+  __shared__ TileRed red;
+  int parity = 0;
+  const int g = blockIdx.x;
+  int t, s0, n;
+  agg_segment(a, g, t, s0, n);
+  if (n == 0) {
+    if (threadIdx.x == 0) a.delta[g] = 1.0f;  // an empty group imposes nothing
+    return;
+  }
+  const size_t base = (size_t)t * a.N + s0;
+  TileLL<PER> ll;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = threadIdx.x + j * kTB;
+    ll.l[j] = ll.valid(j, n) ? a.ll_parent[base + i] - a.ll_child[base + i] : 0.f;
+  }
+  float lm = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (ll.valid(j, n)) lm = fmaxf(lm, ll.l[j]);
+  lm = block_max(lm, &red, parity);
+  const double thr = a.ess_prop * (double)n;
+  auto f = [&](double x) { return block_ess_objective(ll, n, lm, x, thr, &red, parity); };
+  const double top = 1.0 - (double)a.temperature[t];
+  const double ftop = f(top);
+  double delta = top;
+  if (ftop < 0.0) delta = block_brentq(f, 0.0, top, (double)n - thr, ftop);
+  if (threadIdx.x == 0) a.delta[g] = (float)delta;
+}
+
+// inclusive cumsum of buf[0..n) in place: float64 running sum rounded per
+// element to float32 (torch's CPU cumsum), contiguous chunk per thread
+__device__ __forceinline__ void block_cumsum(float* buf, int n, TileRed* red, int& parity) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int chunk = (n + kTB - 1) / kTB;
+  const int b0 = min((int)threadIdx.x * chunk, n), b1 = min(b0 + chunk, n);
+  double part = 0.0;
+  for (int i = b0; i < b1; ++i) part += (double)buf[i];
+  double incl = part;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double y = __shfl_up(incl, o, kWave);
+    if (lane >= o) incl += y;
+  }
+  const int k = parity;
+  parity ^= 1;
+  if (lane == 63) red->d[k][wave][0] = incl;
+  __syncthreads();
+  double run = incl - part;
+  for (int i = 0; i < wave; ++i) run += red->d[k][i][0];
+  for (int i = b0; i < b1; ++i) {
+    run += (double)buf[i];
+    buf[i] = (float)run;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kTB) void agg_reweight_kernel(AggTileArgs a) {
+  extern __shared__ float buf[];  // n floats
+  __shared__ TileRed red;
+  int parity = 0;
+  const int g = blockIdx.x;
+  int t, s0, n;
+  agg_segment(a, g, t, s0, n);
+  // temperature - temperature_prev, float32 tensors (aggregate.py:440-442)
+  const float d = a.temperature[t] - a.temperature_prev[t];
+  if (n == 0) return;
+  const size_t base = (size_t)t * a.N + s0;
+  float mx = -INFINITY;
+  for (int i = threadIdx.x; i < n; i += kTB) {
+    const float e = d * (a.ll_parent[base + i] - a.ll_child[base + i]);
+    a.log_w[base + i] = e;
+    buf[i] = e;
+    mx = fmaxf(mx, e);
+  }
+  mx = block_max(mx, &red, parity);
+  double s = 0.0, unused = 0.0;
+  for (int i = threadIdx.x; i < n; i += kTB) {
+    const float e = expf(buf[i] - mx);
+    buf[i] = e;
+    s += (double)e;
+  }
+  block_sum2(s, unused, &red, parity);
+  const float sf = (float)s;
+  double q = 0.0;
+  for (int i = threadIdx.x; i < n; i += kTB) {
+    const float w = buf[i] / sf;  // softmax within the group (:452-454)
+    a.w_intra[base + i] = w;
+    buf[i] = w;
+    q += (double)w * (double)w;
+  }
+  block_sum2(q, unused, &red, parity);
+  if (threadIdx.x == 0) {
+    a.ess[g] = (float)(1.0 / q);
+    // (wt - wt.max()).exp().mean().log() + wt.max(), added to the group's log Z (:456-465)
+    a.lnc[g] = a.lnc[g] + (logf(sf / (float)n) + mx);
+  }
+  if (!a.idx) return;
+  // ---- intracount multinomial resampling (:506-515), tile-local indices -----
+  block_cumsum(buf, n, &red, parity);
+  const float total = buf[n - 1];
+  for (int i = threadIdx.x; i < n; i += kTB) {
+    float un;
+    if (a.u) {
+      un = a.u[base + i];
+    } else {
+      const uint64_t c = a.offset + (uint64_t)(s0 + i);
+      const U4 r = philox4x32((uint32_t)c, (uint32_t)(c >> 32), (uint32_t)t, kTagAggResample,
+                              a.k0, a.k1);
+      un = u01(r.x);
+    }
+    const float target = un * total;
+    int lo = 0, hi = n;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (buf[mid] > target) hi = mid; else lo = mid + 1;
+    }
+    a.idx[base + i] = (int64_t)(s0 + min(lo, n - 1));
+  }
+}
+
 static int launch_tile(const TileArgs& a, hipStream_t st) {
   if (a.N > kMaxN)
     return set_error(SMCDET_EUNSUPPORTED, "N=%d particles per tile > %d", a.N, kMaxN);
@@ -856,6 +1021,83 @@ int smcdet_count_posterior(const float* log_norm_const, const float* log_count_p
   a.fout = fluxes_out;
   hipLaunchKernelGGL(count_posterior_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("smcdet_count_posterior");
+}
+
+static int agg_tile_common(AggTileArgs& a, const float* loglik_parent,
+                           const float* loglik_children, const float* temperature, int32_t T,
+                           int32_t N, int32_t G, const int32_t* seg_tile,
+                           const int32_t* seg_start, const int32_t* seg_len) {
+  if (!loglik_parent || !loglik_children || !temperature || !seg_tile || !seg_start || !seg_len)
+    return set_error(SMCDET_EINVAL, "null buffer");
+  if (T <= 0 || N <= 0 || G <= 0 || G > 65535 * 64)
+    return set_error(SMCDET_EUNSUPPORTED, "T=%d N=%d G=%d", T, N, G);
+  if (N > kMaxN) return set_error(SMCDET_EUNSUPPORTED, "N=%d particles per tile > %d", N, kMaxN);
+  a.T = T;
+  a.N = N;
+  a.G = G;
+  a.ll_parent = loglik_parent;
+  a.ll_child = loglik_children;
+  a.temperature = temperature;
+  a.seg_tile = seg_tile;
+  a.seg_start = seg_start;
+  a.seg_len = seg_len;
+  return SMCDET_OK;
+}
+
+int smcdet_aggregate_temper(const float* loglik_parent, const float* loglik_children,
+                            const float* temperature, int32_t T, int32_t N, int32_t G,
+                            const int32_t* seg_tile, const int32_t* seg_start,
+                            const int32_t* seg_len, double ess_threshold_prop, float* delta,
+                            void* stream) {
+  AggTileArgs a{};
+  int rc = agg_tile_common(a, loglik_parent, loglik_children, temperature, T, N, G, seg_tile,
+                           seg_start, seg_len);
+  if (rc) return rc;
+  if (!delta) return set_error(SMCDET_EINVAL, "null buffer");
+  a.ess_prop = ess_threshold_prop;
+  a.delta = delta;
+  const int per = (N + kTB - 1) / kTB;
+  const void* fn = per <= 1 ? (const void*)agg_temper_kernel<1>
+                 : per <= 2 ? (const void*)agg_temper_kernel<2>
+                 : per <= 4 ? (const void*)agg_temper_kernel<4>
+                 : per <= 8 ? (const void*)agg_temper_kernel<8>
+                 : per <= 16 ? (const void*)agg_temper_kernel<16>
+                             : (const void*)agg_temper_kernel<32>;
+  void* args[] = {&a};
+  hipError_t e = hipLaunchKernel(fn, dim3(G), dim3(kTB), args, 0, (hipStream_t)stream);
+  if (e != hipSuccess)
+    return set_error(SMCDET_EHIP, "aggregate temper launch: %s", hipGetErrorString(e));
+  return check_launch("smcdet_aggregate_temper");
+}
+
+int smcdet_aggregate_reweight(const float* loglik_parent, const float* loglik_children,
+                              const float* temperature, const float* temperature_prev, int32_t T,
+                              int32_t N, int32_t G, const int32_t* seg_tile,
+                              const int32_t* seg_start, const int32_t* seg_len,
+                              float* log_weights_unnorm, float* weights_intracount,
+                              float* log_norm_const, float* ess, uint64_t seed, uint64_t offset,
+                              const float* u, int64_t* idx, void* stream) {
+  AggTileArgs a{};
+  int rc = agg_tile_common(a, loglik_parent, loglik_children, temperature, T, N, G, seg_tile,
+                           seg_start, seg_len);
+  if (rc) return rc;
+  if (!temperature_prev || !log_weights_unnorm || !weights_intracount || !log_norm_const || !ess)
+    return set_error(SMCDET_EINVAL, "null buffer");
+  a.temperature_prev = temperature_prev;
+  a.log_w = log_weights_unnorm;
+  a.w_intra = weights_intracount;
+  a.lnc = log_norm_const;
+  a.ess = ess;
+  a.k0 = (uint32_t)seed;
+  a.k1 = (uint32_t)(seed >> 32);
+  a.offset = offset;
+  a.u = u;
+  a.idx = idx;
+  const size_t lds = (size_t)N * sizeof(float);
+  rc = ensure_lds((const void*)agg_reweight_kernel, lds + sizeof(TileRed));
+  if (rc) return rc;
+  hipLaunchKernelGGL(agg_reweight_kernel, dim3(G), dim3(kTB), lds, (hipStream_t)stream, a);
+  return check_launch("smcdet_aggregate_reweight");
 }
 
 int smcdet_prune(const float* locs, const float* fluxes, int32_t T, int32_t N, int32_t S,

@@ -56,6 +56,10 @@ class _StrataSampler(SMCsampler):
         self._image_tiles_shape = image_tiles_shape
         self._num_strata = num_strata
 
+    @staticmethod
+    def _particles_per_tile(Prior, num_catalogs):
+        return num_catalogs  # one stratum (count) per stratum tile
+
     def _initial_particles(self):
         nH, nW = self._image_tiles_shape
         N = self.num_catalogs

@@ -47,6 +47,11 @@ class ImageModel(object):
         s = float(self.psf_stdev)
         return torch.exp(-(r ** 2) / (2 * s * s) - math.log(s) - 0.5 * math.log(2 * math.pi))
 
+    def update_psf_grid(self):
+        """Called by Aggregate.join after the tile dimensions change
+        (aggregate.py:241; no reference image model defines it).  The kernels
+        read image_height / image_width on every call: nothing to update."""
+
     # -- C-ABI description -------------------------------------------------
     def _cmodel(self):
         if self.psf_stdev is None:

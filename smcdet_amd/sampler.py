@@ -45,7 +45,7 @@ class SMCsampler(object):
         nt = (image.shape[0] * image.shape[1] if image.dim() == 4
               else (image.shape[0] // tile_dim) ** 2)
         _hip.check_limits(tile_dim, tile_dim, Prior.max_objects,
-                          getattr(Prior, "num_counts", 1) * num_catalogs, nt,
+                          self._particles_per_tile(Prior, num_catalogs), nt,
                           getattr(ImageModel, "psf_radius", None), where="SMCsampler")
         if device is None:
             device = image.device if image.is_cuda else torch.device(
@@ -106,6 +106,11 @@ class SMCsampler(object):
         # optional callback(sampler) after every SMC iteration (e.g. to take a
         # state_dict() checkpoint); runs the loop without speculation
         self.on_iteration = None
+
+    @staticmethod
+    def _particles_per_tile(Prior, num_catalogs):
+        """The stratified initial draw holds num_catalogs particles per count."""
+        return getattr(Prior, "num_counts", 1) * num_catalogs
 
     @classmethod
     def from_tiles(cls, tiles, *args, **kwargs):
@@ -525,6 +530,12 @@ class SMCsampler(object):
         print("done!\n")
 
     # ------------------------------------------------------------ summaries
+    @property
+    def weights_intercount(self):
+        """The final particle weights under the name the reference's drivers
+        pass to Aggregate (experiments/m71/run_smc.py:141-151)."""
+        return self.weights
+
     def posterior_mean_count(self, counts):
         return (self.weights * counts).sum(-1)
 

@@ -1066,6 +1066,125 @@ def gen_cssmc(seeds, smax=4, N=512, K=50):
     print("wrote", path)
 
 
+class JoinableM71ImageModel(M71ImageModel):
+    """The reference M71ImageModel plus the update_psf_grid hook that
+    Aggregate.join calls (aggregate.py:241) and no reference image model
+    defines.  ImageModel.psf reads image_height / image_width on every call
+    (images.py:28-76), so the hook has nothing to update."""
+
+    def update_psf_grid(self):
+        pass
+
+
+def agg_truth_image():
+    """16x16 M71 image of five stars, two near the tile boundaries at 8."""
+    torch.manual_seed(73)
+    l = torch.tensor([[[[[3.2, 4.1], [7.6, 11.3], [12.4, 7.9], [10.8, 13.6], [5.5, 8.4]]]]])
+    f = torch.tensor([[[[6.0, 4.0, 3.0, 1.5, 2.5]]]])
+    m = JoinableM71ImageModel(image_height=16, image_width=16, background=M71["background"],
+                              psf_radius=M71["psf_radius"], adu_per_nmgy=M71["adu_per_nmgy"],
+                              psf_params=torch.tensor(M71["psf_params"]),
+                              noise_additive=M71["noise_additive"],
+                              noise_multiplicative=M71["noise_multiplicative"])
+    return m.sample(l, f)[0, 0, :, :, 0]
+
+
+def agg_inputs(seed, N=48, S=4, H=8, pad=4):
+    """Synthetic 2x2-tile particle populations: counts 0..S, compacted
+    catalogs uniform in the padded tile, fluxes 0.5-20 nmgy."""
+    rng = np.random.default_rng(seed)
+    counts = rng.integers(0, S + 1, (2, 2, N)).astype(np.float32)
+    mask = np.arange(S) < counts[..., None]
+    locs = rng.uniform(-pad, H + pad, (2, 2, N, S, 2)).astype(np.float32) * mask[..., None]
+    fluxes = rng.uniform(0.5, 20.0, (2, 2, N, S)).astype(np.float32) * mask
+    w = rng.random((2, 2, N)).astype(np.float32)
+    w /= w.sum(-1, keepdims=True)
+    lnc = rng.normal(-400.0, 5.0, (2, 2)).astype(np.float32)
+    return counts, locs, fluxes, w, lnc
+
+
+def gen_agg():
+    """The parts of Aggregate (smcdet/aggregate.py) that run at HEAD, on
+    synthetic populations over a 2x2 grid of 8x8 tiles: drop_sources_from_overlap
+    (:189-215), join (:217-263, with JoinableM71ImageModel), unjoin
+    (:265-324), log_target (:105-130), sort_by_count (:424-437), temper
+    (:140-174) and update_weights (:439-483) over two tempering steps."""
+    from smcdet.aggregate import Aggregate
+    torch.manual_seed(0)
+    img = agg_truth_image()
+    data = img.unfold(0, 8, 8).unfold(1, 8, 8).contiguous()
+    counts, locs, fluxes, w, lnc = agg_inputs(5)
+    out = dict(image=np32(img), data=np32(data), counts=counts, locs=locs, fluxes=fluxes,
+               weights=w, lnc=lnc)
+
+    def fresh():
+        model = JoinableM71ImageModel(image_height=8, image_width=8, background=M71["background"],
+                                      psf_radius=M71["psf_radius"],
+                                      adu_per_nmgy=M71["adu_per_nmgy"],
+                                      psf_params=torch.tensor(M71["psf_params"]),
+                                      noise_additive=M71["noise_additive"],
+                                      noise_multiplicative=M71["noise_multiplicative"])
+        mh = SingleComponentMH(10, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+        return Aggregate(m71_prior(8, 0, 4), model, mh, data.clone(), torch.tensor(counts),
+                         torch.tensor(locs), torch.tensor(fluxes), torch.tensor(w),
+                         torch.tensor(lnc), M71["flux_detection_threshold"], "multinomial", 0.5)
+
+    for axis in (0, 1):
+        agg = fresh()
+        c, l, f = agg.drop_sources_from_overlap(axis, torch.tensor(counts), torch.tensor(locs),
+                                                torch.tensor(fluxes))
+        out[f"drop{axis}_counts"], out[f"drop{axis}_locs"], out[f"drop{axis}_fluxes"] = \
+            np32(c), np32(l), np32(f)
+        child_model = __import__("copy").deepcopy(agg.ImageModel)
+        dat, cs, ls, fs = agg.join(axis, agg.data, c, l, f)
+        out[f"join{axis}_data"], out[f"join{axis}_counts"] = np32(dat), np32(cs)
+        out[f"join{axis}_locs"], out[f"join{axis}_fluxes"] = np32(ls), np32(fs)
+        ud, uc, ul, uf = agg.unjoin(axis, dat, ls, fs)
+        out[f"unjoin{axis}_data"], out[f"unjoin{axis}_counts"] = np32(ud), np32(uc)
+        out[f"unjoin{axis}_locs"], out[f"unjoin{axis}_fluxes"] = np32(ul), np32(uf)
+        tau = torch.full((agg.numH, agg.numW), 0.3)
+        lt = agg.log_target(axis, child_model, ud, ul, uf, dat, cs, ls, fs, tau)
+        out[f"logtarget{axis}"] = np32(lt)
+        out[f"logtarget{axis}_tau"] = np32(tau)
+        # two tempering steps over the count groups of the joint population
+        agg.data, agg.counts, agg.locs, agg.fluxes = dat, cs, ls, fs
+        agg.sort_by_count()
+        out[f"sorted{axis}_counts"] = np32(agg.counts)
+        out[f"sorted{axis}_locs"] = np32(agg.locs)
+        out[f"sorted{axis}_fluxes"] = np32(agg.fluxes)
+        groups = agg.num_catalogs_per_count
+        out[f"groups{axis}"] = np.array([[np.array(groups[h][x] + [0] * (8 - len(groups[h][x])))
+                                          for x in range(agg.numW)] for h in range(agg.numH)])
+        ud, uc, ul, uf = agg.unjoin(axis, agg.data, agg.locs, agg.fluxes)
+        lc = child_model.loglikelihood(ud, ul, uf)
+        agg.loglik_diff = agg.ImageModel.loglikelihood(agg.data, agg.locs, agg.fluxes) - \
+            lc.unfold(axis, 2, 2).sum(-1)
+        out[f"loglik_diff{axis}"] = np32(agg.loglik_diff)
+        rng = np.random.default_rng(11 + axis)
+        agg.log_normalizing_constant = [[rng.normal(-300, 3, len(groups[h][x])).tolist()
+                                         for x in range(agg.numW)] for h in range(agg.numH)]
+        out[f"lnc_in{axis}"] = np.array([[np.array(agg.log_normalizing_constant[h][x]
+                                                   + [0.0] * (8 - len(groups[h][x])))
+                                          for x in range(agg.numW)] for h in range(agg.numH)])
+        agg.temperature_prev = torch.zeros(agg.numH, agg.numW)
+        agg.temperature = torch.zeros(agg.numH, agg.numW)
+        for step in (1, 2):
+            if step == 2:  # a second step from tau > 0 with a perturbed increment
+                agg.loglik_diff = agg.loglik_diff * 0.5 + torch.tensor(
+                    rng.normal(0, 2, tuple(agg.loglik_diff.shape)).astype(np.float32))
+                out[f"loglik_diff{axis}_2"] = np32(agg.loglik_diff)
+            agg.temper()
+            agg.update_weights()
+            out[f"tau{axis}_{step}"] = np32(agg.temperature)
+            out[f"w_intra{axis}_{step}"] = np32(agg.weights_intracount)
+            out[f"weights{axis}_{step}"] = np32(agg.weights)
+            out[f"lnc{axis}_{step}"] = np.array([[np.array(
+                [float(v) for v in agg.log_normalizing_constant[h][x]]
+                + [0.0] * (8 - len(groups[h][x]))) for x in range(agg.numW)]
+                for h in range(agg.numH)])
+    save("agg_m71_pieces.npz", **out)
+
+
 if __name__ == "__main__":
     torch.set_default_dtype(torch.float32)
     what = sys.argv[1] if len(sys.argv) > 1 else "fixtures"
@@ -1081,6 +1200,7 @@ if __name__ == "__main__":
         gen_mala()
         gen_mcmc()
         gen_mcmc_edge()
+        gen_agg()
     elif what == "mala":
         gen_mala()
     elif what == "mh-edge":
@@ -1091,6 +1211,8 @@ if __name__ == "__main__":
         gen_mcmc()
     elif what == "mcmc-edge":
         gen_mcmc_edge()
+    elif what == "agg":
+        gen_agg()
     elif what == "cssmc":
         n = int(sys.argv[2]) if len(sys.argv) > 2 else 16
         gen_cssmc(list(range(n)))
