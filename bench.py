@@ -322,7 +322,8 @@ def bench_mcmc(args, dev, rank, world):
         tdist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        on_dev = os.environ.get("SMCDET_DIST_BACKEND", "nccl") == "nccl"
+        t = torch.tensor([elapsed], device=dev if on_dev else "cpu", dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t)
     iters = B * (total - 1)
@@ -457,11 +458,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("SMCDET_DIST_BACKEND", "nccl") != "nccl":
+        local %= max(torch.cuda.device_count(), 1)  # rehearsal: ranks may share a GPU
     dist = world > 1
+    # backend "nccl" (= RCCL on ROCm) for the driver's multi-GPU runs;
+    # SMCDET_DIST_BACKEND=gloo rehearses the same code path with several ranks
+    # sharing one GPU (RCCL refuses two ranks on one device)
+    backend = os.environ.get("SMCDET_DIST_BACKEND", "nccl")
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
     dev = torch.device("cuda", local if dist else 0)
     torch.cuda.set_device(dev)
 
@@ -503,7 +513,8 @@ def main():
         tdist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu",
+                         dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t)
     mh_ms = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
