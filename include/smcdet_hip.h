@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 11
+#define SMCDET_ABI_VERSION 12
 
 /* status codes */
 #define SMCDET_OK 0
@@ -160,18 +160,28 @@ int smcdet_sample_image(const smcdet_image_model_t* model, const float* rate,
                         int64_t count, uint64_t seed, uint64_t offset,
                         float* image, void* stream);
 
+/* Per-tile location boxes (every function taking `tile_boxes`): a nullable
+ * [T,4] float array (lo_h, lo_w, hi_h, hi_w) that replaces the prior's
+ * [-pad, H+pad) x [-pad, W+pad) for tile t -- the tiles' boxes then partition
+ * the padded image (padding only on its outer edges), so the product of the
+ * tiles' priors is the whole image's prior (used by tile aggregation,
+ * DESIGN.md §9).  An M71 prior's Poisson count mean scales with the box
+ * area.  Null: the reference's per-tile padding (prior.py:17-23). */
+
 /* Prior.log_prob (smcdet/prior.py:67-75, :183-189, :220-226): out[T,N]. */
 int smcdet_log_prior(const smcdet_prior_t* prior, const float* counts,
                      const float* locs, const float* fluxes, int32_t T,
-                     int32_t N, int32_t S, float* out, void* stream);
+                     int32_t N, int32_t S, const float* tile_boxes, float* out,
+                     void* stream);
 
 /* Prior.sample(stratify_by_count=True, num_catalogs_per_count=n_per_count)
  * (smcdet/prior.py:25-64, :201-217): N = (max-min+1)*n_per_count.
  * uloc [T,N,S,2] / uflux [T,N,S] replay the uniforms when non-null. */
 int smcdet_prior_sample(const smcdet_prior_t* prior, int32_t T,
                         int32_t n_per_count, uint64_t seed, uint64_t offset,
-                        const float* uloc, const float* uflux, float* counts,
-                        float* locs, float* fluxes, void* stream);
+                        const float* uloc, const float* uflux,
+                        const float* tile_boxes, float* counts, float* locs,
+                        float* fluxes, void* stream);
 
 /* SingleComponentMH.run (smcdet/kernel.py:26-130), K = mh->num_iters
  * iterations fused in one launch.  Reads the state of particle
@@ -193,7 +203,8 @@ int smcdet_prior_sample(const smcdet_prior_t* prior, int32_t T,
  * exactly; rate_in != rate_out when ancestors is non-null.
  * go (nullable, int32 device scalar): when *go == 0 the launch does nothing
  * (no output is written) -- lets a host enqueue the next SMC iteration before
- * it has read the loop condition (see smcdet_temper_reweight's `live`). */
+ * it has read the loop condition (see smcdet_temper_reweight's `live`).
+ * tile_boxes (nullable): per-tile location boxes in place of mh->locs_min/max. */
 int smcdet_mh_sweep(const smcdet_image_model_t* model,
                     const smcdet_prior_t* prior, const smcdet_mh_t* mh,
                     const float* tiled_image, const float* temperature,
@@ -204,7 +215,8 @@ int smcdet_mh_sweep(const smcdet_image_model_t* model,
                     float* rate_out, uint64_t seed,
                     uint64_t offset, const smcdet_mh_replay_t* replay,
                     uint32_t flags, float* loglik_out, float* acc_rate,
-                    int32_t* acc_count, const int32_t* go, void* stream);
+                    int32_t* acc_count, const int32_t* go,
+                    const float* tile_boxes, void* stream);
 
 /* SingleComponentMALA.run (smcdet/kernel.py:133-275), K iterations fused in
  * one launch.  Arguments as smcdet_mh_sweep; mala->locs_stdev and
@@ -310,6 +322,7 @@ int smcdet_gather(const int64_t* idx, int32_t T, int32_t N, int32_t S,
  * Per image tile t, with NS count strata k (count s_min + k) whose fixed-count
  * samplers ran as "stratum tiles" t*NS + k of N equally weighted particles:
  *   probs[t,k] = p(s|x) = softmax_k(log_norm_const[t*NS+k] + log_count_prior[k])
+ *   (log_count_prior [T,NS] per tile when lcp_per_tile != 0: tile boxes)
  *   then n_out catalogs: stratum k_n ~ probs[t,:] (systematic: u_n = (n+U)/n_out,
  *   first k with cumsum(probs) >= u_n; multinomial: iid u_n), and a uniform
  *   particle m_n = floor(v_n * N) of that stratum; idx[t,n] = k_n*N + m_n and
@@ -318,7 +331,8 @@ int smcdet_gather(const int64_t* idx, int32_t T, int32_t N, int32_t S,
  * u_strata ([T] systematic / [T,n_out] multinomial) and u_pick [T,n_out]
  * replay the uniforms when non-null. */
 int smcdet_count_posterior(const float* log_norm_const,
-                           const float* log_count_prior, int32_t T, int32_t NS,
+                           const float* log_count_prior, int32_t lcp_per_tile,
+                           int32_t T, int32_t NS,
                            int32_t N, int32_t S, int32_t n_out,
                            int32_t resample_method, uint64_t seed,
                            uint64_t offset, const float* u_strata,
@@ -352,7 +366,8 @@ int smcdet_prune(const float* locs, const float* fluxes, int32_t T, int32_t N,
  * returned state, from a fresh render (num_iters = 0 evaluates the input
  * state).  acc_rate [T] (nullable) = acceptance rate of the last iteration,
  * with acc_count [2T] as in smcdet_mh_sweep.  Replay layout as
- * smcdet_mh_replay_t (comp must be < count). */
+ * smcdet_mh_replay_t (comp must be < count).  tile_boxes (nullable): per
+ * joint tile location boxes in place of mh->locs_min/max. */
 int smcdet_aggregate_sweep(const smcdet_image_model_t* model,
                            const smcdet_prior_t* prior, const smcdet_mh_t* mh,
                            int32_t axis, const float* tiled_image,
@@ -363,7 +378,8 @@ int smcdet_aggregate_sweep(const smcdet_image_model_t* model,
                            float* locs_out, float* fluxes_out, uint64_t seed,
                            uint64_t offset, const smcdet_mh_replay_t* replay,
                            float* loglik_parent, float* loglik_children,
-                           float* acc_rate, int32_t* acc_count, void* stream);
+                           float* acc_rate, int32_t* acc_count,
+                           const float* tile_boxes, void* stream);
 
 /* Aggregate.temper (aggregate.py:140-174), per count group: the particles of
  * each joint tile are sorted by count and split into G segments (count

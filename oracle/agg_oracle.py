@@ -157,7 +157,7 @@ def agg_mh_sweep(data, counts, locs, fluxes, tau, prior, model, axis, mh, comp, 
     locs = np.array(locs, dtype=dtype)
     fluxes = np.array(fluxes, dtype=dtype)
     K = comp.shape[0]
-    lb_l = dtype(prior.loc_low)
+    lb_l = np.asarray(prior.loc_low, dtype=dtype)
     ub_l = np.array(prior.loc_high, dtype=dtype)
     sl, sf = dtype(mh.locs_stdev), dtype(mh.fluxes_stdev)
     lb_f, ub_f = dtype(mh.fluxes_min), dtype(mh.fluxes_max)

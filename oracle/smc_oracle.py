@@ -86,7 +86,10 @@ class BasicModel:
 
 @dataclass
 class M71PriorP:
-    """smcdet/prior.py:192-226 (M71Prior) over PoissonProcessPrior :78-101."""
+    """smcdet/prior.py:192-226 (M71Prior) over PoissonProcessPrior :78-101.
+    box = (lo_h, lo_w, hi_h, hi_w) replaces [-pad, H+pad) x [-pad, W+pad)
+    (a tile's own box when the tiles partition the padded image; the Poisson
+    mean is counts_rate times the box area, as for the padded tile)."""
     min_objects: int
     max_objects: int
     counts_rate: float
@@ -96,16 +99,24 @@ class M71PriorP:
     flux_alpha: float
     flux_lower: float
     flux_upper: float
+    box: tuple = None
 
     @property
     def loc_low(self):
+        if self.box is not None:
+            return np.array([_f32(self.box[0]), _f32(self.box[1])])
         return _f32(-self.pad)
 
     @property
     def loc_high(self):
+        if self.box is not None:
+            return (_f32(self.box[2]), _f32(self.box[3]))
         return (_f32(self.H + self.pad), _f32(self.W + self.pad))
 
     def poisson_mean(self):
+        if self.box is not None:
+            b = self.box
+            return _f32(self.counts_rate * (b[2] - b[0]) * (b[3] - b[1]))
         return _f32(self.counts_rate * (self.H + 2 * self.pad) * (self.W + 2 * self.pad))
 
 
@@ -272,7 +283,7 @@ def log_prior(counts, locs, fluxes, prior, dtype=np.float64):
         k = prior.max_objects - prior.min_objects + 1
         insup = (counts >= prior.min_objects) & (counts <= prior.max_objects)
         lp = np.where(insup, dtype(np.log(np.float32(1.0 / k))), -np.inf)
-    lo = dtype(prior.loc_low)
+    lo = np.asarray(prior.loc_low, dtype=dtype)
     hi = np.array(prior.loc_high, dtype=dtype)
     inside = (locs >= lo) & (locs < hi)
     lu = np.where(inside, -np.log(hi - lo), -np.inf)  # Uniform.log_prob
@@ -300,7 +311,7 @@ def prior_sample_stratified(prior, num_tiles_per_side, n_per_count, uloc, uflux,
     counts = (strata * np.ones((T, T, strata.size))).astype(dtype)
     S = prior.max_objects
     mask = np.arange(S)[None] < counts[..., None]
-    lo = dtype(prior.loc_low)
+    lo = np.asarray(prior.loc_low, dtype=dtype)
     hi = np.array(prior.loc_high, dtype=dtype)
     locs = lo + np.asarray(uloc, dtype=dtype) * (hi - lo)
     locs = locs * mask[..., None]
@@ -365,7 +376,7 @@ def mh_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mh,
     locs = np.array(locs, dtype=dtype)
     fluxes = np.array(fluxes, dtype=dtype)
     K = comp.shape[0]
-    lb_l = dtype(prior.loc_low)
+    lb_l = np.asarray(prior.loc_low, dtype=dtype)
     ub_l = np.array(prior.loc_high, dtype=dtype)
     sl, sf = dtype(mh.locs_stdev), dtype(mh.fluxes_stdev)
     lb_f, ub_f = dtype(mh.fluxes_min), dtype(mh.fluxes_max)

@@ -23,7 +23,7 @@ SMCDET_RESAMPLE_SYSTEMATIC = 1
 SMCDET_MH_FULL_RECOMPUTE = 1
 SMCDET_MH_COMPONENT_BY_COUNT = 2
 SMCDET_MH_SKIP_DONE = 4
-ABI_VERSION = 11
+ABI_VERSION = 12
 SMCDET_SMC_FREEZE_DONE = 1
 
 # Shapes the kernels support (checked by the C ABI too; the samplers raise
@@ -95,10 +95,12 @@ _SIGS = {
     "smcdet_render": ([c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
     "smcdet_psf_dense": ([c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
     "smcdet_sample_image": ([c_p, c_p, c_i64, c_u64, c_u64, c_p, c_p], c_i),
-    "smcdet_log_prior": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
-    "smcdet_prior_sample": ([c_p, c_i, c_i, c_u64, c_u64, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
+    "smcdet_log_prior": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p], c_i),
+    "smcdet_prior_sample": ([c_p, c_i, c_i, c_u64, c_u64, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
+                            c_i),
     "smcdet_mh_sweep": ([c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p,
-                         c_p, c_p, c_p, c_u64, c_u64, c_p, c_u32, c_p, c_p, c_p, c_p, c_p], c_i),
+                         c_p, c_p, c_p, c_u64, c_u64, c_p, c_u32, c_p, c_p, c_p, c_p, c_p, c_p],
+                        c_i),
     "smcdet_mala_sweep": ([c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p,
                            c_p, c_p, c_p, c_u64, c_u64, c_p, c_u32, c_p, c_p, c_p, c_p, c_p],
                           c_i),
@@ -110,11 +112,12 @@ _SIGS = {
     "smcdet_temper_reweight": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_d, c_i, c_u64,
                                 c_u64, c_p, c_u32, c_p, c_i, c_p, c_p, c_p, c_p], c_i),
     "smcdet_gather": ([c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
-    "smcdet_count_posterior": ([c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_u64, c_u64, c_p, c_p,
-                                c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
+    "smcdet_count_posterior": ([c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_u64, c_u64, c_p,
+                                c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
     "smcdet_prune": ([c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p, c_p, c_p, c_p], c_i),
     "smcdet_aggregate_sweep": ([c_p, c_p, c_p, c_i, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p,
-                                c_p, c_p, c_p, c_u64, c_u64, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
+                                c_p, c_p, c_p, c_u64, c_u64, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
+                               c_i),
     "smcdet_aggregate_temper": ([c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_d, c_p, c_p],
                                 c_i),
     "smcdet_aggregate_reweight": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p,

@@ -53,6 +53,7 @@ import torch
 from . import _hip
 from ._rng import PhiloxStream
 from .kernel import SingleComponentMALA
+from .prior import partition_boxes
 
 
 def _f32(t):
@@ -155,12 +156,13 @@ class CountGroups(object):
 
 def aggregate_sweep(image_model, prior, mh, axis, data, temperature, counts, locs, fluxes, *,
                     num_iters=None, ancestors=None, replay=None, seed=0, offset=0,
-                    acc_workspace=None):
+                    acc_workspace=None, tile_boxes=None):
     """One smcdet_aggregate_sweep launch on joint tiles data [numH,numW,H,W]
     (image_model / prior at the joint dimensions, mh a SingleComponentMH):
     num_iters (default mh.num_iters) MH iterations on the bridging target.
     Returns (counts, locs, fluxes, loglik_parent, loglik_children, acc_rate);
-    acc_rate is None without acc_workspace ([2T] zeroed int32)."""
+    acc_rate is None without acc_workspace ([2T] zeroed int32).  tile_boxes
+    [T,4] (optional): each joint tile's own location box."""
     data = _hip.dev_f32(data, "data")
     locs = _hip.dev_f32(locs, "locs")
     fluxes = _hip.dev_f32(fluxes, "fluxes")
@@ -187,12 +189,15 @@ def aggregate_sweep(image_model, prior, mh, axis, data, temperature, counts, loc
                           _hip.ptr(ru[2]).value)
     if ancestors is not None:
         ancestors = ancestors.to(device=dev, dtype=torch.int64).contiguous()
+    if tile_boxes is not None:
+        tile_boxes = _hip.dev_f32(tile_boxes.to(dev), "tile_boxes")
     _hip.check(_hip.lib().smcdet_aggregate_sweep(
         _hip.ref(image_model._cmodel()), _hip.ref(prior._cprior()), _hip.ref(ch), int(axis),
         _hip.ptr(data), _hip.ptr(temperature), T, N, S, _hip.ptr(ancestors), _hip.ptr(counts),
         _hip.ptr(locs), _hip.ptr(fluxes), _hip.ptr(co), _hip.ptr(lo), _hip.ptr(lf), int(seed),
         int(offset), _hip.ref(rp) if rp is not None else None, _hip.ptr(lp), _hip.ptr(lc),
-        _hip.ptr(acc), _hip.ptr(acc_workspace), _hip.stream_of(lo)), "smcdet_aggregate_sweep")
+        _hip.ptr(acc), _hip.ptr(acc_workspace), _hip.ptr(tile_boxes), _hip.stream_of(lo)),
+        "smcdet_aggregate_sweep")
     del keep
     return co, lo, lf, lp, lc, acc
 
@@ -313,11 +318,24 @@ class Aggregate(object):
         self._pending_idx = None
         self._acc_ws = None
         self.loglik_parent = self.loglik_children = None
+        # Prior pad_mode "partition" (the tiles' boxes partition the padded
+        # image): nothing to drop at a merge, and every joint tile keeps the
+        # partition box of its place in the grid -- the exact variant of §9
+        self.partition = getattr(self.Prior, "pad_mode", "tile") == "partition"
 
     # ------------------------------------------------------------ bookkeeping
     @property
     def _T(self):
         return self.numH * self.numW
+
+    @property
+    def tile_boxes(self):
+        """[T,4] location boxes of the current (joint) tiles in partition
+        mode, else None (every tile uses the prior's padded box)."""
+        if not self.partition:
+            return None
+        return partition_boxes((self.numH, self.numW), self.dimH, self.dimW, self.Prior.pad,
+                               self.device)
 
     def _build_segments(self, counts_sorted):
         self._groups = CountGroups(counts_sorted)
@@ -380,7 +398,8 @@ class Aggregate(object):
                    parent_counts, parent_locs, parent_fluxes, temperature):
         """aggregate.py:105-130 (host helper; the sweep evaluates it in-kernel).
         child_* in unjoin's layout (children of joint tile i at 2i, 2i+1)."""
-        logprior = self.Prior.log_prob(parent_counts, parent_locs, parent_fluxes)
+        logprior = self.Prior.log_prob(parent_counts, parent_locs, parent_fluxes,
+                                       tile_boxes=self.tile_boxes)
         child = ChildImageModel.loglikelihood(child_data, child_locs, child_fluxes)
         child = _axis_sel(child, axis, 0) + _axis_sel(child, axis, 1)
         parent = self.ImageModel.loglikelihood(parent_data, parent_locs, parent_fluxes)
@@ -416,13 +435,13 @@ class Aggregate(object):
          self.mutation_acc_rates) = aggregate_sweep(
             self.ImageModel, self.Prior, self.MutationKernel, axis, self.data, self.temperature,
             self.counts, self.locs, self.fluxes, ancestors=anc, seed=self.rng.seed, offset=off,
-            acc_workspace=self._acc_ws)
+            acc_workspace=self._acc_ws, tile_boxes=self.tile_boxes)
 
     def evaluate(self, axis):
         """l_p and l_c1 + l_c2 of the current state (the sweep with K = 0)."""
         _, _, _, self.loglik_parent, self.loglik_children, _ = aggregate_sweep(
             self.ImageModel, self.Prior, self.MutationKernel, axis, self.data, self.temperature,
-            self.counts, self.locs, self.fluxes, num_iters=0)
+            self.counts, self.locs, self.fluxes, num_iters=0, tile_boxes=self.tile_boxes)
         return self.loglik_parent, self.loglik_children
 
     @property
@@ -493,7 +512,8 @@ class Aggregate(object):
         child_lz = self.log_evidence
         index = self.get_resampled_index(self.weights, 1)
         cs, ls, fs, _ = self.apply_resampled_index(index, self.counts, self.locs, self.fluxes)
-        cs, ls, fs = self.drop_sources_from_overlap(axis, cs, ls, fs)
+        if not self.partition:  # partition boxes do not overlap: nothing to drop
+            cs, ls, fs = self.drop_sources_from_overlap(axis, cs, ls, fs)
         self.data, self.counts, self.locs, self.fluxes = self.join(axis, self.data, cs, ls, fs)
         self._child_log_evidence = _axis_sel(child_lz, axis, 0) + _axis_sel(child_lz, axis, 1)
 

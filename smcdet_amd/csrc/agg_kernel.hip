@@ -66,6 +66,7 @@ struct AggArgs {
   float* ll_child;
   int32_t* acc_count;
   float* acc_rate;
+  const float* boxes;  // [T,4] per-joint-tile location boxes (or null)
   const int32_t* r_comp;
   const float* r_uloc;
   const float* r_uflux;
@@ -175,8 +176,12 @@ __global__ __launch_bounds__(kAggMaxWaves* kWave) void agg_sweep_kernel(AggArgs 
   // lane d < 3 proposes dimension d (h, w, flux); lanes >= 3 shadow dimension 2
   const int d = min(lane, 2);
   const float isig = d < 2 ? a.isl : a.isf, sig = d < 2 ? a.sl : a.sf;
-  const float lb = d == 0 ? a.lb_h : (d == 1 ? a.lb_w : a.lb_f);
-  const float ub = d == 0 ? a.ub_h : (d == 1 ? a.ub_w : a.ub_f);
+  float lb = d == 0 ? a.lb_h : (d == 1 ? a.lb_w : a.lb_f);
+  float ub = d == 0 ? a.ub_h : (d == 1 ? a.ub_w : a.ub_f);
+  if (a.boxes && d < 2) {  // the joint tile's own box (partition of the padded image)
+    lb = a.boxes[4 * t + d];
+    ub = a.boxes[4 * t + 2 + d];
+  }
   const float scale = m.g * psf_scale<MODEL>(m);
   const float omt = 1.0f - tau;
 
@@ -324,7 +329,8 @@ extern "C" int smcdet_aggregate_sweep(
     int32_t S, const int64_t* ancestors, const float* counts_in, const float* locs_in,
     const float* fluxes_in, float* counts_out, float* locs_out, float* fluxes_out, uint64_t seed,
     uint64_t offset, const smcdet_mh_replay_t* replay, float* loglik_parent,
-    float* loglik_children, float* acc_rate, int32_t* acc_count, void* stream) {
+    float* loglik_children, float* acc_rate, int32_t* acc_count, const float* tile_boxes,
+    void* stream) {
   int rc = validate_model(model);
   if (rc) return rc;
   rc = validate_prior(prior);
@@ -385,6 +391,7 @@ extern "C" int smcdet_aggregate_sweep(
   a.ll_child = loglik_children;
   a.acc_count = acc_count;
   a.acc_rate = acc_rate;
+  a.boxes = tile_boxes;
   if (replay) {
     a.r_comp = replay->comp;
     a.r_uloc = replay->uloc;

@@ -82,6 +82,7 @@ DevPrior make_dev_prior(const smcdet_prior_t& p) {
   DevPrior d{};
   d.kind = p.kind;
   d.lo = p.loc_low;
+  d.lo_w = p.loc_low;
   d.hi_h = p.loc_high_h;
   d.hi_w = p.loc_high_w;
   d.min_objects = p.min_objects;

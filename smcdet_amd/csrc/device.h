@@ -415,7 +415,8 @@ __device__ __forceinline__ float erfinv_fast(float x) {
 
 struct DevPrior {
   int kind;
-  float lo, hi_h, hi_w;
+  float lo, hi_h, hi_w;      // location box: [lo, hi_h) x [lo_w, hi_w)
+  float lo_w;
   float count_c0, count_c1;  // M71: log(mu), mu ; PARETO: log(1/k), unused
   int min_objects, max_objects;
   float flux_c;              // log-normaliser of the flux density
@@ -426,6 +427,24 @@ struct DevPrior {
 
 DevPrior make_dev_prior(const smcdet_prior_t& p);  // common.hip
 int validate_prior(const smcdet_prior_t* p);        // common.hip
+
+// A tile's own location box (lo_h, lo_w, hi_h, hi_w) in place of the
+// prior's [-pad, H+pad) x [-pad, W+pad): the uniform densities follow the
+// box, and a Poisson count mean scales with its area (M71: the mean is
+// counts_rate times the padded tile area, prior.py:91-97)
+__device__ __forceinline__ void tile_box_prior(DevPrior& pr, const float* b) {
+  const float area0 = (pr.hi_h - pr.lo) * (pr.hi_w - pr.lo_w);
+  pr.lo = b[0];
+  pr.lo_w = b[1];
+  pr.hi_h = b[2];
+  pr.hi_w = b[3];
+  pr.loc_lp_h = -logf(pr.hi_h - pr.lo);
+  pr.loc_lp_w = -logf(pr.hi_w - pr.lo_w);
+  if (pr.kind == SMCDET_PRIOR_M71) {
+    pr.count_c1 = pr.count_c1 * ((pr.hi_h - pr.lo) * (pr.hi_w - pr.lo_w) / area0);
+    pr.count_c0 = logf(pr.count_c1);
+  }
+}
 
 // ---------------------------------------------------------------------------
 // LDS image staging: x and (Poisson) lgamma(x+1) for one tile

@@ -74,6 +74,7 @@ struct MhArgs {
   const float* rate_in;              // [T,N,H*W] persisted rate images or null
   float* rate_out;                   // [T,N,H*W] or null
   const int32_t* go;                 // predicate: skip the launch when *go == 0 (or null)
+  const float* boxes;                // [T,4] per-tile location boxes (or null: lb_*/ub_*)
   int32_t* acc_count;                // [2T] zeroed workspace: counts, tickets
   float* acc_rate;                   // [T]
   const int32_t* r_comp;             // replay (or null)
@@ -308,8 +309,18 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   Dim dm;
   dm.isig = d < 2 ? a.isl : a.isf;
   dm.sig = d < 2 ? a.sl : a.sf;
-  dm.lb = d == 0 ? a.lb_h : (d == 1 ? a.lb_w : a.lb_f);
-  dm.ub = d == 0 ? a.ub_h : (d == 1 ? a.ub_w : a.ub_f);
+  {
+    float lb_h = a.lb_h, lb_w = a.lb_w, ub_h = a.ub_h, ub_w = a.ub_w;
+    if (a.boxes) {  // the tile's own box (a partition of the padded image)
+      const float* bx_ = a.boxes + 4 * t;
+      lb_h = bx_[0];
+      lb_w = bx_[1];
+      ub_h = bx_[2];
+      ub_w = bx_[3];
+    }
+    dm.lb = d == 0 ? lb_h : (d == 1 ? lb_w : a.lb_f);
+    dm.ub = d == 0 ? ub_h : (d == 1 ? ub_w : a.ub_f);
+  }
   const bool ablate_prop = (a.ablate & SMCDET_MH_ABLATE_PROPOSAL) != 0;
   const bool ablate_lik = (a.ablate & SMCDET_MH_ABLATE_LIKELIHOOD) != 0;
 
@@ -778,7 +789,7 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
                                float* rate_out, uint64_t seed,
                                uint64_t offset, const smcdet_mh_replay_t* replay, uint32_t flags,
                                float* loglik_out, float* acc_rate, int32_t* acc_count,
-                               const int32_t* go, void* stream) {
+                               const int32_t* go, const float* tile_boxes, void* stream) {
   int rc = validate_model(model);
   if (rc) return rc;
   rc = validate_prior(prior);
@@ -835,6 +846,7 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
   a.acc_count = acc_count;
   a.acc_rate = acc_rate;
   a.go = go;
+  a.boxes = tile_boxes;
   if (replay) {
     a.r_comp = replay->comp;
     a.r_uloc = replay->uloc;

@@ -160,12 +160,17 @@ __global__ void sample_image_kernel(DevModel m, const float* __restrict__ rate, 
 // ---------------------------------------------------------------------------
 // M71Prior.log_prob (prior.py:220-226, :67-75) / ParetoStarPrior.log_prob
 // (prior.py:183-189): thread per particle
+// tile_boxes [T,4] (lo_h, lo_w, hi_h, hi_w), nullable: per-tile location boxes
+// (a partition of the padded image, SMCDET_ABI 12); the Poisson count mean
+// scales with the box area
 __global__ void log_prior_kernel(DevPrior pr, const float* __restrict__ counts,
                                  const float* __restrict__ locs, const float* __restrict__ fluxes,
-                                 int64_t TN, int S, float* __restrict__ out) {
+                                 int64_t TN, int N, int S, const float* __restrict__ boxes,
+                                 float* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= TN) return;
   const float c = counts[i];
+  if (boxes) tile_box_prior(pr, boxes + 4 * (i / N));
   float lp;
   if (pr.kind == SMCDET_PRIOR_M71) {
     lp = c * pr.count_c0 - pr.count_c1 - lgammaf(c + 1.0f);  // Poisson.log_prob
@@ -178,7 +183,7 @@ __global__ void log_prior_kernel(DevPrior pr, const float* __restrict__ counts,
     if (!((float)s < c)) break;  // counts_mask
     const float h = locs[(i * S + s) * 2 + 0], w = locs[(i * S + s) * 2 + 1];
     const float lh = (h >= pr.lo && h < pr.hi_h) ? pr.loc_lp_h : -INFINITY;
-    const float lw = (w >= pr.lo && w < pr.hi_w) ? pr.loc_lp_w : -INFINITY;
+    const float lw = (w >= pr.lo_w && w < pr.hi_w) ? pr.loc_lp_w : -INFINITY;
     sl += lh + lw;
     float f = fluxes[i * S + s];
     if (f == 0.f) f = pr.lower;
@@ -191,13 +196,14 @@ __global__ void log_prior_kernel(DevPrior pr, const float* __restrict__ counts,
 __global__ void prior_sample_kernel(DevPrior pr, int T, int N, int n_per_count, int S,
                                     uint32_t k0, uint32_t k1, uint64_t offset,
                                     const float* __restrict__ uloc, const float* __restrict__ uflux,
-                                    float* __restrict__ counts, float* __restrict__ locs,
-                                    float* __restrict__ fluxes) {
+                                    const float* __restrict__ boxes, float* __restrict__ counts,
+                                    float* __restrict__ locs, float* __restrict__ fluxes) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)T * N * S) return;
   const int s = (int)(i % S);
   const int64_t tn = i / S;
   const int n = (int)(tn % N);
+  if (boxes) tile_box_prior(pr, boxes + 4 * (tn / N));
   const float c = (float)(pr.min_objects + n / n_per_count);
   if (s == 0) counts[tn] = c;
   float uh, uw, uf;
@@ -218,7 +224,7 @@ __global__ void prior_sample_kernel(DevPrior pr, int T, int N, int n_per_count, 
   const bool on = (float)s < c;
   // Uniform(low, high).rsample: low + u*(high - low)
   const float h = fmaf(uh, pr.hi_h - pr.lo, pr.lo);
-  const float w = fmaf(uw, pr.hi_w - pr.lo, pr.lo);
+  const float w = fmaf(uw, pr.hi_w - pr.lo_w, pr.lo_w);
   float f;
   if (pr.kind == SMCDET_PRIOR_M71) {
     // TruncatedPareto.sample (distributions.py:76-85)
@@ -347,8 +353,8 @@ int smcdet_sample_image(const smcdet_image_model_t* model, const float* rate, in
 }
 
 int smcdet_log_prior(const smcdet_prior_t* prior, const float* counts, const float* locs,
-                     const float* fluxes, int32_t T, int32_t N, int32_t S, float* out,
-                     void* stream) {
+                     const float* fluxes, int32_t T, int32_t N, int32_t S,
+                     const float* tile_boxes, float* out, void* stream) {
   int rc = validate_prior(prior);
   if (rc) return rc;
   if (!counts || !locs || !fluxes || !out) return set_error(SMCDET_EINVAL, "null buffer");
@@ -356,13 +362,14 @@ int smcdet_log_prior(const smcdet_prior_t* prior, const float* counts, const flo
   const DevPrior d = make_dev_prior(*prior);
   const int64_t TN = (int64_t)T * N;
   hipLaunchKernelGGL(log_prior_kernel, dim3((unsigned)((TN + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, d, counts, locs, fluxes, TN, S, out);
+                     (hipStream_t)stream, d, counts, locs, fluxes, TN, N, S, tile_boxes, out);
   return check_launch("smcdet_log_prior");
 }
 
 int smcdet_prior_sample(const smcdet_prior_t* prior, int32_t T, int32_t n_per_count,
                         uint64_t seed, uint64_t offset, const float* uloc, const float* uflux,
-                        float* counts, float* locs, float* fluxes, void* stream) {
+                        const float* tile_boxes, float* counts, float* locs, float* fluxes,
+                        void* stream) {
   int rc = validate_prior(prior);
   if (rc) return rc;
   if (!counts || !locs || !fluxes) return set_error(SMCDET_EINVAL, "null buffer");
@@ -382,7 +389,7 @@ int smcdet_prior_sample(const smcdet_prior_t* prior, int32_t T, int32_t n_per_co
   }
   hipLaunchKernelGGL(prior_sample_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                      d, T, N, n_per_count, S, (uint32_t)seed, (uint32_t)(seed >> 32), offset, uloc,
-                     uflux, counts, locs, fluxes);
+                     uflux, tile_boxes, counts, locs, fluxes);
   return check_launch("smcdet_prior_sample");
 }
 

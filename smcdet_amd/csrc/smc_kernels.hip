@@ -607,7 +607,8 @@ struct CountPostArgs {
   uint32_t k0, k1;
   uint64_t offset;
   const float* logZ;
-  const float* lcp;
+  const float* lcp;          // [NS], or [T,NS] with lcp_per_tile
+  int lcp_per_tile;
   const float* u_strata;
   const float* u_pick;
   const float* cin;
@@ -625,15 +626,16 @@ __global__ __launch_bounds__(256) void count_posterior_kernel(CountPostArgs a) {
   __shared__ double U;
   const int t = blockIdx.x;
   const int NS = a.NS;
+  const float* lcp = a.lcp + (a.lcp_per_tile ? (size_t)t * NS : 0);
   if (threadIdx.x == 0) {
     double m = -INFINITY;
     for (int k = 0; k < NS; ++k)
-      m = fmax(m, (double)a.logZ[(size_t)t * NS + k] + (double)a.lcp[k]);
+      m = fmax(m, (double)a.logZ[(size_t)t * NS + k] + (double)lcp[k]);
     double s = 0.0;
-    for (int k = 0; k < NS; ++k) s += exp((double)a.logZ[(size_t)t * NS + k] + (double)a.lcp[k] - m);
+    for (int k = 0; k < NS; ++k) s += exp((double)a.logZ[(size_t)t * NS + k] + (double)lcp[k] - m);
     double c = 0.0;
     for (int k = 0; k < NS; ++k) {
-      const double p = exp((double)a.logZ[(size_t)t * NS + k] + (double)a.lcp[k] - m) / s;
+      const double p = exp((double)a.logZ[(size_t)t * NS + k] + (double)lcp[k] - m) / s;
       a.probs[(size_t)t * NS + k] = (float)p;
       c += p;
       cdf[k] = c;
@@ -980,8 +982,9 @@ int smcdet_gather(const int64_t* idx, int32_t T, int32_t N, int32_t S, const flo
   return check_launch("smcdet_gather");
 }
 
-int smcdet_count_posterior(const float* log_norm_const, const float* log_count_prior, int32_t T,
-                           int32_t NS, int32_t N, int32_t S, int32_t n_out,
+int smcdet_count_posterior(const float* log_norm_const, const float* log_count_prior,
+                           int32_t lcp_per_tile, int32_t T, int32_t NS, int32_t N, int32_t S,
+                           int32_t n_out,
                            int32_t resample_method, uint64_t seed, uint64_t offset,
                            const float* u_strata, const float* u_pick, const float* counts_in,
                            const float* locs_in, const float* fluxes_in, float* probs,
@@ -1009,6 +1012,7 @@ int smcdet_count_posterior(const float* log_norm_const, const float* log_count_p
   a.offset = offset;
   a.logZ = log_norm_const;
   a.lcp = log_count_prior;
+  a.lcp_per_tile = lcp_per_tile != 0;
   a.u_strata = u_strata;
   a.u_pick = u_pick;
   a.cin = counts_in;

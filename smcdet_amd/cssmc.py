@@ -51,10 +51,15 @@ class _StrataSampler(SMCsampler):
     """SMCsampler over the [numH, numW*NS] stratum tiles: the initial draw is
     the stratified prior draw of each image tile, split by count."""
 
-    def __init__(self, *args, image_tiles_shape, num_strata, **kwargs):
+    def __init__(self, *args, image_tiles_shape, num_strata, image_tile_boxes=None, **kwargs):
+        # the strata of image tile t are stratum tiles t*NS .. t*NS+NS-1: they
+        # share the image tile's location box
+        if image_tile_boxes is not None:
+            kwargs["tile_boxes"] = image_tile_boxes.repeat_interleave(num_strata, dim=0)
         super().__init__(*args, **kwargs)
         self._image_tiles_shape = image_tiles_shape
         self._num_strata = num_strata
+        self._image_tile_boxes = image_tile_boxes
 
     @staticmethod
     def _particles_per_tile(Prior, num_catalogs):
@@ -64,7 +69,8 @@ class _StrataSampler(SMCsampler):
         nH, nW = self._image_tiles_shape
         N = self.num_catalogs
         c, l, f = self.Prior.sample_stratified(nH, N, device=self.device, rng=self.rng,
-                                               tiles_shape=(nH, nW))
+                                               tiles_shape=(nH, nW),
+                                               tile_boxes=self._image_tile_boxes)
         # [nH, nW, NS*N, ...] (counts in blocks of N, prior.py:47-54) -> stratum tiles
         S = l.shape[-2]
         T2 = nW * self._num_strata
@@ -116,12 +122,21 @@ class CountStratifiedSMC(object):
         NS = self.num_strata
         strata_tiles = (self.tiled_image.unsqueeze(2).expand(nH, nW, NS, tile_dim, tile_dim)
                         .reshape(nH, nW * NS, tile_dim, tile_dim).contiguous())
+        # Prior pad_mode "partition": each image tile its own location box
+        boxes = sampler_kwargs.pop("tile_boxes", None)
+        if boxes is None and hasattr(Prior, "tile_boxes"):
+            boxes = Prior.tile_boxes((nH, nW), self.device)
+        self.tile_boxes = boxes
         self.sampler = _StrataSampler(
             strata_tiles, tile_dim, Prior, ImageModel, mh, num_catalogs_per_count,
             ess_threshold_prop, resample_method, flux_detection_threshold, max_smc_iters,
             print_every, seed=seed, device=self.device, image_tiles_shape=(nH, nW),
-            num_strata=NS, **sampler_kwargs)
-        self.log_count_prior = log_count_prior(Prior).to(self.device)
+            num_strata=NS, image_tile_boxes=boxes, **sampler_kwargs)
+        if boxes is None:
+            self.log_count_prior = log_count_prior(Prior).to(self.device)
+        else:  # [T, NS]: a Poisson count mean scales with the tile's box area
+            self.log_count_prior = Prior.log_count_prior_per_tile(boxes).to(
+                device=self.device, dtype=torch.float32).contiguous()
         self.has_run = False
 
     def _per_tile(self, x, *rest):
@@ -149,7 +164,8 @@ class CountStratifiedSMC(object):
             u_strata = _hip.dev_f32(u_strata.to(self.device), "u_strata")
             u_pick = _hip.dev_f32(u_pick.to(self.device), "u_pick")
         _hip.check(_hip.lib().smcdet_count_posterior(
-            _hip.ptr(logZ), _hip.ptr(self.log_count_prior), T, NS, N, S, n_out, method,
+            _hip.ptr(logZ), _hip.ptr(self.log_count_prior), int(self.log_count_prior.dim() == 2),
+            T, NS, N, S, n_out, method,
             s.rng.seed, off, _hip.ptr(u_strata), _hip.ptr(u_pick), _hip.ptr(s.counts),
             _hip.ptr(s.locs), _hip.ptr(s.fluxes), _hip.ptr(probs), _hip.ptr(idx),
             _hip.ptr(counts), _hip.ptr(locs), _hip.ptr(fluxes), _hip.stream_of(probs)),
@@ -160,7 +176,9 @@ class CountStratifiedSMC(object):
         self.weights = torch.full((nH, nW, n_out), 1.0 / n_out, device=self.device)
         lz = logZ.reshape(nH, nW, NS)
         self.log_normalizing_constant_per_count = lz
-        self.log_normalizing_constant = torch.logsumexp(lz + self.log_count_prior, -1)
+        lcp = self.log_count_prior.reshape(nH, nW, NS) if self.log_count_prior.dim() == 2 \
+            else self.log_count_prior
+        self.log_normalizing_constant = torch.logsumexp(lz + lcp, -1)
         self.pruned_counts, self.pruned_locs, self.pruned_fluxes = s.prune(locs, fluxes)
 
     def run(self):

@@ -96,7 +96,7 @@ class SingleComponentMH(object):
 
     def run(self, data, counts, locs, fluxes, temperature, log_target=None, *, prior=None,
             image_model=None, ancestors=None, replay=None, want_loglik=True, rate_in=None,
-            rate_out=None, flags=0, go=None):
+            rate_out=None, flags=0, go=None, tile_boxes=None):
         """kernel.py:26-130.  ancestors [numH,numW,N] (int64, optional) gathers
         the starting state (a fused resample); replay = dict(comp, uloc, uflux,
         uacc) replays recorded draws; rate_in / rate_out [numH,numW,N,H*W]
@@ -104,7 +104,8 @@ class SingleComponentMH(object):
         images of (locs, fluxes), rate_out receives those of the result
         (ignored in full_recompute mode).  go (int32 device scalar, optional):
         the launch does nothing when *go == 0 (speculative enqueue, see
-        SMCsampler.run)."""
+        SMCsampler.run).  tile_boxes [T,4] (optional): each tile's own
+        location box (Prior pad_mode "partition")."""
         prior, image_model = self._resolve(log_target, prior, image_model)
         data = _hip.dev_f32(data, "data")
         counts = _hip.dev_f32(counts, "counts")
@@ -145,6 +146,14 @@ class SingleComponentMH(object):
         if self.component_by_count:
             flags |= _hip.SMCDET_MH_COMPONENT_BY_COUNT
         flags |= int(extra_flags)
+        extra = []
+        if self._entry == "smcdet_mh_sweep":
+            if tile_boxes is not None:
+                tile_boxes = _hip.dev_f32(tile_boxes.to(dev), "tile_boxes")
+            extra = [_hip.ptr(tile_boxes)]
+        elif tile_boxes is not None:
+            raise NotImplementedError(f"{type(self).__name__}: per-tile location boxes "
+                                      "(pad_mode='partition') need SingleComponentMH")
         ev = self.launch_events
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -157,7 +166,7 @@ class SingleComponentMH(object):
             _hip.ptr(self._rate_buffer(rate_out, "rate_out", T * N, data)),
             self.rng.seed, off,
             _hip.ref(rp) if rp is not None else None, flags, _hip.ptr(ll), _hip.ptr(acc),
-            _hip.ptr(acc_ws), _hip.ptr(go), _hip.stream_of(locs)), self._entry)
+            _hip.ptr(acc_ws), _hip.ptr(go), *extra, _hip.stream_of(locs)), self._entry)
         if ev is not None:
             e1.record(torch.cuda.current_stream(dev))
             ev.append((e0, e1))

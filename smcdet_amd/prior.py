@@ -24,6 +24,28 @@ def _f32(x):
     return float(np.float32(x))
 
 
+def _check_pad_mode(mode):
+    if mode not in ("tile", "partition"):
+        raise ValueError("pad_mode must be either tile or partition.")
+    return mode
+
+
+def partition_boxes(tiles_shape, tile_h, tile_w, pad, device=None):
+    """[numH*numW, 4] float32 (lo_h, lo_w, hi_h, hi_w) per tile, in tile
+    coordinates: [0, H) x [0, W), widened by `pad` on the sides that are the
+    image's outer edges."""
+    nH, nW = tiles_shape
+    i = torch.arange(nH, dtype=torch.float32).reshape(nH, 1).expand(nH, nW)
+    j = torch.arange(nW, dtype=torch.float32).reshape(1, nW).expand(nH, nW)
+    p = float(pad)
+    lo_h = torch.where(i == 0, -p, 0.0)
+    lo_w = torch.where(j == 0, -p, 0.0)
+    hi_h = torch.where(i == nH - 1, tile_h + p, float(tile_h))
+    hi_w = torch.where(j == nW - 1, tile_w + p, float(tile_w))
+    b = torch.stack([lo_h, lo_w, hi_h, hi_w], -1).reshape(nH * nW, 4)
+    return b.to(device=device).contiguous()
+
+
 def _device(device=None):
     if device is not None:
         return torch.device(device)
@@ -35,14 +57,23 @@ def _device(device=None):
 
 class PointProcessPrior(object):
     """prior.py:8-75: discrete-uniform count, uniform locations over the
-    padded tile [-pad, H+pad) x [-pad, W+pad)."""
+    padded tile [-pad, H+pad) x [-pad, W+pad).
 
-    def __init__(self, min_objects, max_objects, image_height, image_width, pad=0):
+    pad_mode (keyword-only extension): "tile" (the reference: every tile of an
+    image is padded on all four sides, so neighbouring tiles' boxes overlap)
+    or "partition" (only the image's outer edges are padded: the tiles' boxes
+    partition the padded image, and the product of the tiles' priors is the
+    whole image's prior -- what tile aggregation needs to be exact,
+    DESIGN.md §9)."""
+
+    def __init__(self, min_objects, max_objects, image_height, image_width, pad=0, *,
+                 pad_mode="tile"):
         self.min_objects = min_objects
         self.max_objects = max_objects
         self.image_height = image_height
         self.image_width = image_width
         self.pad = pad
+        self.pad_mode = _check_pad_mode(pad_mode)
         self.update_attrs()
 
     def update_attrs(self):
@@ -52,6 +83,28 @@ class PointProcessPrior(object):
             (0 - self.pad) * torch.ones(2, device="cpu"),
             torch.tensor((self.image_height + self.pad, self.image_width + self.pad),
                          dtype=torch.float32, device="cpu"))
+
+    def tile_boxes(self, tiles_shape, device=None):
+        """Per-tile location boxes for a numH x numW grid of image tiles of
+        this prior's size: None with pad_mode "tile" (every tile uses the
+        prior's own box), else partition_boxes()."""
+        if getattr(self, "pad_mode", "tile") == "tile":
+            return None
+        return partition_boxes(tiles_shape, self.image_height, self.image_width, self.pad,
+                               device)
+
+    def log_count_prior_per_tile(self, boxes):
+        """log p(s), s = min..max, per tile box [T, NS]: a Poisson count mean
+        scales with the box area (prior.py:91-97)."""
+        s = torch.arange(self.min_objects, self.max_objects + 1, dtype=torch.float64)
+        b = boxes.detach().cpu().double()
+        if isinstance(self, PoissonProcessPrior):
+            area = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
+            mu = torch.tensor([_f32(self.counts_rate * float(a)) for a in area],
+                              dtype=torch.float64)[:, None]
+            return s * torch.log(mu) - mu - torch.lgamma(s + 1)
+        return torch.full((b.shape[0], s.numel()), -float(np.log(s.numel())),
+                          dtype=torch.float64)
 
     # --- C-ABI description ----------------------------------------------------
     def _cprior(self):
@@ -104,11 +157,12 @@ class PointProcessPrior(object):
 
     def sample_stratified(self, num_tiles_per_side, num_catalogs_per_count, device=None,
                           rng: PhiloxStream | None = None, uloc=None, uflux=None,
-                          tiles_shape=None):
+                          tiles_shape=None, tile_boxes=None):
         """Stratified draw on device: counts = min..max (each repeated
         num_catalogs_per_count times), uniform locs, prior fluxes, masked past
         each count.  uloc/uflux replay the reference's torch.rand draws.
-        tiles_shape=(numH, numW) overrides the square num_tiles_per_side grid."""
+        tiles_shape=(numH, numW) overrides the square num_tiles_per_side grid;
+        tile_boxes [T,4] (optional) gives each tile its own location box."""
         device = _device(device)
         nH, nW = tiles_shape if tiles_shape is not None else (num_tiles_per_side,) * 2
         N = self.num_counts * num_catalogs_per_count
@@ -122,22 +176,28 @@ class PointProcessPrior(object):
         if uloc is not None:
             uloc = _hip.dev_f32(uloc.to(device), "uloc")
             uflux = _hip.dev_f32(uflux.to(device), "uflux")
+        if tile_boxes is not None:
+            tile_boxes = _hip.dev_f32(tile_boxes.to(device), "tile_boxes")
         _hip.check(_hip.lib().smcdet_prior_sample(
             _hip.ref(cp), nH * nW, num_catalogs_per_count, rng.seed, off, _hip.ptr(uloc),
-            _hip.ptr(uflux), _hip.ptr(counts), _hip.ptr(locs), _hip.ptr(fluxes),
-            _hip.stream_of(counts)), "smcdet_prior_sample")
+            _hip.ptr(uflux), _hip.ptr(tile_boxes), _hip.ptr(counts), _hip.ptr(locs),
+            _hip.ptr(fluxes), _hip.stream_of(counts)), "smcdet_prior_sample")
         return counts, locs, fluxes
 
-    def log_prob(self, counts, locs, fluxes):
-        """prior.py:67-75 (+ flux terms of :183-189 / :220-226): [numH,numW,N]."""
+    def log_prob(self, counts, locs, fluxes, *, tile_boxes=None):
+        """prior.py:67-75 (+ flux terms of :183-189 / :220-226): [numH,numW,N].
+        tile_boxes [T,4] (optional): each tile's own location box."""
         counts = _hip.dev_f32(counts, "counts")
         locs = _hip.dev_f32(locs, "locs")
         fluxes = _hip.dev_f32(fluxes, "fluxes")
         nH, nW, n, d, _ = locs.shape
         out = torch.empty(nH, nW, n, device=locs.device, dtype=torch.float32)
         cp = self._cprior()
+        if tile_boxes is not None:
+            tile_boxes = _hip.dev_f32(tile_boxes.to(locs.device), "tile_boxes")
         _hip.check(_hip.lib().smcdet_log_prior(_hip.ref(cp), _hip.ptr(counts), _hip.ptr(locs),
-                                               _hip.ptr(fluxes), nH * nW, n, d, _hip.ptr(out),
+                                               _hip.ptr(fluxes), nH * nW, n, d,
+                                               _hip.ptr(tile_boxes), _hip.ptr(out),
                                                _hip.stream_of(locs)), "smcdet_log_prior")
         self.counts_mask = torch.arange(d, device=counts.device) < counts.unsqueeze(-1)
         return out
@@ -146,13 +206,15 @@ class PointProcessPrior(object):
 class PoissonProcessPrior(PointProcessPrior):
     """prior.py:78-101: Poisson(counts_rate * (H+2pad)(W+2pad)) count prior."""
 
-    def __init__(self, min_objects, max_objects, counts_rate, image_height, image_width, pad=0):
+    def __init__(self, min_objects, max_objects, counts_rate, image_height, image_width, pad=0, *,
+                 pad_mode="tile"):
         self.min_objects = min_objects
         self.max_objects = max_objects
         self.counts_rate = counts_rate
         self.image_height = image_height
         self.image_width = image_width
         self.pad = pad
+        self.pad_mode = _check_pad_mode(pad_mode)
         self.update_attrs()
 
     def update_attrs(self):

@@ -39,7 +39,7 @@ class SMCsampler(object):
     def __init__(self, image, tile_dim, Prior, ImageModel, MutationKernel, num_catalogs,
                  ess_threshold_prop, resample_method, flux_detection_threshold, max_smc_iters,
                  print_every=5, *, seed=None, device=None, fused=True, persist_rate_images=True,
-                 rate_refresh_every=8, stopping="lockstep"):
+                 rate_refresh_every=8, stopping="lockstep", tile_boxes=None):
         # shapes the kernels cannot run raise here, naming the limit (before
         # anything touches the device)
         nt = (image.shape[0] * image.shape[1] if image.dim() == 4
@@ -62,6 +62,16 @@ class SMCsampler(object):
             self.tiled_image = (self.image.unfold(0, self.tile_dim, self.tile_dim)
                                 .unfold(1, self.tile_dim, self.tile_dim).contiguous())
         self.tiles_shape = tuple(self.tiled_image.shape[:2])
+        # per-tile location boxes [T,4]: explicit, or from the prior's pad_mode
+        # ("partition": only the image's outer edges padded)
+        if tile_boxes is None:
+            tile_boxes = Prior.tile_boxes(self.tiles_shape, self.device) \
+                if hasattr(Prior, "tile_boxes") else None
+        self.tile_boxes = (None if tile_boxes is None else
+                           tile_boxes.to(self.device, torch.float32).reshape(-1, 4).contiguous())
+        if self.tile_boxes is not None and self.tile_boxes.shape[0] != self.tiles_shape[0] * \
+                self.tiles_shape[1]:
+            raise ValueError("tile_boxes must hold one (lo_h, lo_w, hi_h, hi_w) row per tile")
 
         self.Prior = Prior
         self.ImageModel = ImageModel
@@ -141,7 +151,8 @@ class SMCsampler(object):
         """Stratified prior draw (prior.py:25-64): [numH,numW,N,...]."""
         return self.Prior.sample_stratified(self.tiles_shape[0], self.num_catalogs,
                                             device=self.device, rng=self.rng,
-                                            tiles_shape=self.tiles_shape)
+                                            tiles_shape=self.tiles_shape,
+                                            tile_boxes=self.tile_boxes)
 
     def initialize(self):
         """sampler.py:57-85."""
@@ -165,7 +176,7 @@ class SMCsampler(object):
 
     def log_target(self, data, counts, locs, fluxes, temperature):
         """sampler.py:87-91."""
-        logprior = self.Prior.log_prob(counts, locs, fluxes)
+        logprior = self.Prior.log_prob(counts, locs, fluxes, tile_boxes=self.tile_boxes)
         loglik = self.ImageModel.loglikelihood(data, locs, fluxes)
         return logprior + temperature.unsqueeze(-1) * loglik
 
@@ -266,6 +277,8 @@ class SMCsampler(object):
             kw["flags"] = _hip.SMCDET_MH_SKIP_DONE
         if getattr(self, "_go", None) is not None:
             kw["go"] = self._go
+        if self.tile_boxes is not None:
+            kw["tile_boxes"] = self.tile_boxes
         self.locs, self.fluxes, self.mutation_acc_rates = self.MutationKernel.run(
             self.tiled_image, self.counts, self.locs, self.fluxes, self.temperature,
             self.log_target, ancestors=ancestors, **kw)

@@ -28,6 +28,24 @@ def test_every_header_symbol_is_exported_and_bound():
     assert set(names) == set(_hip.EXPORTS), set(names) ^ set(_hip.EXPORTS)
 
 
+def header_arity():
+    """name -> number of parameters, from the header's declarations."""
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(smcdet_[a-z_0-9]+)\s*\(([^;{]*?)\)\s*;", txt, re.S):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
+def test_ctypes_signatures_match_header_arity():
+    """Every binding passes exactly as many arguments as the header declares
+    (a mismatch would shift pointers into the wrong parameters)."""
+    arity = header_arity()
+    for name, (args, _) in _hip._SIGS.items():
+        assert arity[name] == len(args), (name, arity[name], len(args))
+
+
 def test_version_and_abi():
     assert _hip.lib().smcdet_abi_version() == _hip.ABI_VERSION
     assert "gfx950" in _hip.version()

@@ -3,7 +3,6 @@ path: shard arithmetic, tile splitting, the end-of-run catalog gather and the
 lockstep stopping collective.  The HIP kernels are not called (no GPU here);
 the per-rank sampler state is synthetic."""
 import os
-import socket
 
 import pytest
 import torch
@@ -35,17 +34,17 @@ def test_split_tiles_row_major():
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A fresh file:// rendezvous for one process group (no TCP port to race
+    for between picking it and binding it)."""
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="smcdet_gloo_")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
 def _worker(rank, world, port, num_tiles, tps, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
     try:
         a, b = shard_tiles(num_tiles, world, rank)
         T = b - a
@@ -58,7 +57,9 @@ def _worker(rank, world, port, num_tiles, tps, q):
         }
         out = gather_tile_results(local, num_tiles, tps, rank, world, dst=0)
         if rank == 0:
-            q.put({k: v.clone() for k, v in out.items()})
+            # numpy, not tensors: a tensor sent through a torch.multiprocessing
+            # queue is fetched from the sender's process, which may have exited
+            q.put({k: v.numpy().copy() for k, v in out.items()})
         else:
             assert out is None
 
@@ -76,16 +77,14 @@ def _worker(rank, world, port, num_tiles, tps, q):
 
 
 def _worker_images(rank, world, port, num_images, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
     try:
         a, b = shard_tiles(num_images, world, rank)
         ids = torch.arange(a, b, dtype=torch.float32)
         local = {"log_normalizing_constant": -ids, "counts": ids[:, None].repeat(1, 4),
                  "num_iters": ids + 1}
         out = gather_tile_results(local, num_images, None, rank, world, dst=0)
-        q.put(out if rank == 0 else None)
+        q.put({k: v.numpy().copy() for k, v in out.items()} if rank == 0 else None)
     finally:
         dist.destroy_process_group()
 
@@ -103,7 +102,7 @@ def test_gather_independent_images_gloo():
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    full = next(g for g in got if g is not None)
+    full = {k: torch.as_tensor(v) for k, v in next(g for g in got if g is not None).items()}
     ids = torch.arange(num_images, dtype=torch.float32)
     assert torch.equal(full["log_normalizing_constant"], -ids)
     assert full["counts"].shape == (num_images, 4)
@@ -124,7 +123,7 @@ def test_gather_and_lockstep_gloo(world):
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    full = next(g for g in got if isinstance(g, dict))
+    full = {k: torch.as_tensor(v) for k, v in next(g for g in got if isinstance(g, dict)).items()}
     keeps = [g for g in got if isinstance(g, tuple)]
     idx = torch.arange(num_tiles, dtype=torch.float32).reshape(tps, tps)
     assert torch.equal(full["counts"][..., 0], idx)

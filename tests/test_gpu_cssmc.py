@@ -50,7 +50,7 @@ def test_count_posterior_kernel_vs_oracle(method):
         _hip.SMCDET_RESAMPLE_MULTINOMIAL
     keep = [d(logZ), d(lcp), d(us), d(up), d(counts), d(locs), d(fluxes)]
     _hip.check(_hip.lib().smcdet_count_posterior(
-        *[_hip.ptr(k) for k in keep[:2]], T, NS, Np, S, n_out, m, 0, 0,
+        *[_hip.ptr(k) for k in keep[:2]], 0, T, NS, Np, S, n_out, m, 0, 0,
         *[_hip.ptr(k) for k in keep[2:]], _hip.ptr(probs), _hip.ptr(idx), _hip.ptr(co),
         _hip.ptr(lo), _hip.ptr(fo), _hip.stream_of(probs)), "count_posterior")
     p_ref = O.count_posterior(logZ, lcp)
