@@ -67,7 +67,10 @@ def parse():
     # mcmc: the reference's MCMC baseline (MHsampler, experiments/m71/
     # run_mcmc.py: 8x8 M71 cutouts, S=10, 50,000 samples, burn-in 30,000,
     # every 2nd kept), one chain per image, a batch of images per GPU
-    ap.add_argument("--workload", choices=["c2", "c4", "c5", "mcmc"], default="c2")
+    # agg: tile aggregation (smcdet/aggregate.py): CS-SMC on the
+    # 4x4 8x8 tiles of a 32x32 image (partition boxes, pad 2, counts 0..6),
+    # then Aggregate over 4 levels to one 32x32 population; one image per GPU
+    ap.add_argument("--workload", choices=["c2", "c4", "c5", "mcmc", "agg"], default="c2")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--particles", type=int, default=4096)
@@ -282,6 +285,82 @@ def build_sampler(args, dev, rank):
         mh_iters=K, kernel=args.kernel)
 
 
+def bench_agg(args, dev, rank, world):
+    """Aggregate.run() on one synthetic 32x32 M71 image per GPU, after
+    count-stratified SMC on its 4x4 grid of 8x8 tiles (untimed).  value =
+    aggregation MH particle-steps (sum over levels of joint tiles x N x K x
+    SMC iterations) / the run's wall time."""
+    import contextlib
+    import io
+    from smcdet_amd.aggregate import Aggregate
+    from smcdet_amd.cssmc import CountStratifiedSMC
+    from smcdet_amd.kernel import SingleComponentMH
+    from smcdet_amd.prior import M71Prior
+    p = M71
+    H, tile, N, K = 32, 8, args.particles, args.mh_iters
+    model32, _, truth = make_models(H, 10)
+    model8, _, _ = make_models(tile, 10)
+    kp = M71Prior(min_objects=0, max_objects=6, counts_rate=COUNTS_RATE_C2, image_height=tile,
+                  image_width=tile, flux_alpha=p["flux_alpha"], flux_lower=p["flux_lower"],
+                  flux_upper=p["flux_upper"], pad=2, pad_mode="partition")
+    torch.manual_seed(3000 + rank)
+    while True:
+        c, l, f = truth.sample(num_catalogs=1, device=dev)
+        if int(c.reshape(-1)[0]) <= 10:
+            break
+    img = model32.sample(l, f)[0, 0, :, :, 0].contiguous()
+
+    def mh():
+        return SingleComponentMH(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"])
+
+    def one(seed):
+        kids = CountStratifiedSMC(img, tile, kp, model8, mh(), N, 0.5, "systematic",
+                                  p["flux_detection_threshold"], 200, print_every=10 ** 9,
+                                  num_catalogs=N, seed=seed, device=dev)
+        with contextlib.redirect_stdout(io.StringIO()):
+            kids.run()
+        agg = Aggregate(kp, model8, mh(), kids.tiled_image, kids.counts, kids.locs, kids.fluxes,
+                        kids.weights, kids.log_normalizing_constant,
+                        p["flux_detection_threshold"], "systematic", 0.5, print_every=10 ** 9,
+                        seed=seed + 1, device=dev)
+        torch.cuda.synchronize()
+        if world > 1:
+            import torch.distributed as tdist
+            tdist.barrier()
+        t0 = time.perf_counter()
+        with contextlib.redirect_stdout(io.StringIO()):
+            agg.run()
+        torch.cuda.synchronize()
+        if world > 1:
+            tdist.barrier()
+        return agg, time.perf_counter() - t0
+    one(11 + 100 * rank)  # warm-up
+    agg, elapsed = one(12 + 100 * rank)
+    if world > 1:
+        import torch.distributed as tdist
+        on_dev = os.environ.get("SMCDET_DIST_BACKEND", "nccl") == "nccl"
+        t = torch.tensor([elapsed], device=dev if on_dev else "cpu", dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t)
+    tiles_per_level = [(H // tile) ** 2 // 2 ** (lv + 1) for lv in range(agg.num_aggregation_levels)]
+    steps = sum(t * it for t, it in zip(tiles_per_level, agg.iters_per_level)) * N * K
+    return {
+        "metric": "aggregation MH particle-steps/sec (agg workload: 4x4 8x8 tiles -> 32x32)",
+        "value": world * steps / elapsed, "unit": "particle-steps/sec", "n_gpus": world,
+        "steps": 1, "warmup": 1, "ms_per_step": elapsed * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (M71 prior + image model, seed 3000+rank)",
+        "config": {"workload": f"AGG: one 32x32 M71 image/GPU, CS-SMC on 4x4 8x8 tiles (counts "
+                               f"0..6, pad 2 partition), Aggregate N={N}, K={K}",
+                   "particles": N, "mh_iters": K, "levels": agg.num_aggregation_levels,
+                   "parallelism": f"image-sharded x{world}"},
+        "aggregate": {"iters_per_level": agg.iters_per_level, "joint_tiles_per_level":
+                      tiles_per_level, "final_sources": int(agg.locs.shape[-2]),
+                      "log_evidence": float(agg.log_evidence.reshape(-1)[0]),
+                      "detected_mean": float(agg.pruned_counts.float().mean())},
+    }
+
+
 def bench_mcmc(args, dev, rank, world):
     """MHsampler over a batch of 8x8 M71 cutouts (one chain each): the whole
     run() is timed, as run_mcmc.py:121-125 times it per image."""
@@ -475,10 +554,10 @@ def main():
     dev = torch.device("cuda", local if dist else 0)
     torch.cuda.set_device(dev)
 
-    if args.workload != "c2" and args.tiles_per_gpu == 1:
+    if args.workload not in ("c2", "agg") and args.tiles_per_gpu == 1:
         args.tiles_per_gpu = 42  # 332 M71 cutouts over 8 GPUs (manuscript.tex:562)
-    if args.workload == "mcmc":
-        out = bench_mcmc(args, dev, rank, world)
+    if args.workload in ("mcmc", "agg"):
+        out = (bench_mcmc if args.workload == "mcmc" else bench_agg)(args, dev, rank, world)
         if rank == 0:
             print(json.dumps(out), flush=True)
         if dist:
