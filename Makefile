@@ -4,7 +4,7 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 CSRC := smcdet_amd/csrc
 SRCS := $(CSRC)/common.hip $(CSRC)/model_kernels.hip $(CSRC)/mh_kernel.hip $(CSRC)/mala_kernel.hip $(CSRC)/chain_kernel.hip $(CSRC)/smc_kernels.hip $(CSRC)/agg_kernel.hip
-HDRS := $(CSRC)/device.h $(CSRC)/render.h $(CSRC)/mcmc.h include/smcdet_hip.h
+HDRS := $(CSRC)/device.h $(CSRC)/render.h $(CSRC)/mcmc.h $(CSRC)/tile.h include/smcdet_hip.h
 OBJS := $(SRCS:.hip=.o)
 LIB := smcdet_amd/libsmcdet_hip.so
 # build provenance: sha1 of the sources in this order (smcdet_amd/_hip.py

@@ -93,6 +93,9 @@ def parse():
     ap.add_argument("--no-full-run", action="store_true")
     # skip the untimed comparison with the reference's recorded runs
     ap.add_argument("--no-vs-ref", action="store_true")
+    # A/B: the sweep and the temper/reweight/resample pass as two launches
+    # instead of one fused launch (SMCsampler.fused_step)
+    ap.add_argument("--split-step", action="store_true")
     return ap.parse_args()
 
 
@@ -532,6 +535,15 @@ def _full_run(s2):
     return time.perf_counter() - t0
 
 
+def _hip_fused(s):
+    """Whether smcdet_mh_sweep_step runs this sampler's shapes as one launch."""
+    from smcdet_amd import _hip
+    mh = s.MutationKernel
+    flags = _hip.SMCDET_MH_FULL_RECOMPUTE if getattr(mh, "full_recompute", False) else 0
+    return bool(_hip.lib().smcdet_mh_sweep_step_fused(
+        _hip.ref(s.ImageModel._cmodel()), int(s.counts.shape[-1]), int(s.locs.shape[-2]), flags))
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -564,15 +576,19 @@ def main():
             tdist.destroy_process_group()
         return
     s, mh, steps_per_step, cpu_tile, cfg = build_sampler(args, dev, rank)
+    s.fused_step = not args.split_step
     s.initialize()
+    cfg = dict(cfg, step="split" if args.split_step else (
+        "fused" if s._step_fusable() and _hip_fused(s) else "split (shape)"))
     s._temper_reweight(with_resample=True)
 
     ev = []
 
     def step():
+        # one SMC iteration: the MH sweep from the ancestors, then temper /
+        # reweight / next indices in the same launch (SMCsampler._step)
         idx, s._pending_idx = s._pending_idx, None
-        s.mutate(ancestors=idx)
-        s._temper_reweight(with_resample=True)
+        s._step(idx)
 
     for _ in range(args.warmup):
         step()

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 12
+#define SMCDET_ABI_VERSION 13
 
 /* status codes */
 #define SMCDET_OK 0
@@ -310,6 +310,59 @@ int smcdet_temper_reweight(const float* loglik, float* temperature,
                            uint64_t offset, int64_t* idx, uint32_t flags,
                            int32_t* finished_iter, int32_t iter, int32_t* live,
                            const int32_t* go, int32_t* live_host, void* stream);
+
+/* The temper / reweight / resample-index half of a fused SMC iteration
+ * (smcdet_mh_sweep_step): the arguments of smcdet_temper_reweight that the
+ * sweep does not already carry (its loglik_out and temperature are the
+ * pass's log-likelihoods and temperatures).  resample_u [T] (nullable)
+ * replays the systematic offsets (tests); multinomial draws are not
+ * replayable here. */
+typedef struct smcdet_smc_tail {
+  float* temperature_prev;
+  float* log_weights_unnorm;
+  float* weights;
+  float* ess;
+  float* log_norm_const;
+  double ess_threshold;
+  int32_t resample_method;
+  uint32_t flags;            /* SMCDET_SMC_* */
+  uint64_t seed;
+  uint64_t offset;
+  int64_t* idx;              /* [T,N] next resampling indices (nullable) */
+  const float* resample_u;   /* [T] systematic U replay (nullable) */
+  int32_t* finished_iter;
+  int32_t* live;
+  int32_t* live_host;
+  int32_t iter;
+  int32_t reserved;
+} smcdet_smc_tail_t;
+
+/* One SMC iteration of SMCsampler.run (smcdet/sampler.py:221-237: resample
+ * -> mutate -> temper -> update_weights, the resample being the sweep's
+ * ancestor gather): smcdet_mh_sweep followed by smcdet_temper_reweight on its
+ * loglik_out (required), with the same results bit for bit.  One launch: the
+ * last workgroup to finish a tile runs the tile's temper / reweight / index
+ * pass in the sweep's own LDS, so the pass starts the moment the tile's last
+ * particle is done and the step pays one launch instead of two.  Shapes the
+ * fused form does not cover (N % 4 != 0, N > 4096, tiles of <= 64 pixels,
+ * SMCDET_MH_FULL_RECOMPUTE, an LDS budget that would cost occupancy) run as
+ * the two launches; smcdet_mh_sweep_step_fused() reports which. */
+int smcdet_mh_sweep_step(const smcdet_image_model_t* model,
+                         const smcdet_prior_t* prior, const smcdet_mh_t* mh,
+                         const float* tiled_image, float* temperature,
+                         int32_t T, int32_t N, int32_t S,
+                         const int64_t* ancestors, const float* counts_in,
+                         const float* locs_in, const float* fluxes_in,
+                         float* counts_out, float* locs_out, float* fluxes_out,
+                         const float* rate_in, float* rate_out, uint64_t seed,
+                         uint64_t offset, const smcdet_mh_replay_t* replay,
+                         uint32_t flags, float* loglik_out, float* acc_rate,
+                         int32_t* acc_count, const int32_t* go,
+                         const float* tile_boxes, const smcdet_smc_tail_t* tail,
+                         void* stream);
+/* 1 when smcdet_mh_sweep_step runs these shapes as one launch, else 0. */
+int smcdet_mh_sweep_step_fused(const smcdet_image_model_t* model, int32_t N,
+                               int32_t S, uint32_t flags);
 
 /* Gather of the resampled state (smcdet/sampler.py:150-169). */
 int smcdet_gather(const int64_t* idx, int32_t T, int32_t N, int32_t S,

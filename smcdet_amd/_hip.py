@@ -23,7 +23,7 @@ SMCDET_RESAMPLE_SYSTEMATIC = 1
 SMCDET_MH_FULL_RECOMPUTE = 1
 SMCDET_MH_COMPONENT_BY_COUNT = 2
 SMCDET_MH_SKIP_DONE = 4
-ABI_VERSION = 12
+ABI_VERSION = 13
 SMCDET_SMC_FREEZE_DONE = 1
 
 # Shapes the kernels support (checked by the C ABI too; the samplers raise
@@ -85,6 +85,16 @@ class ReplayC(ctypes.Structure):
     _fields_ = [("comp", c_p), ("uloc", c_p), ("uflux", c_p), ("uacc", c_p)]
 
 
+class SmcTailC(ctypes.Structure):
+    """smcdet_smc_tail_t: the temper / reweight / resample-index half of a
+    fused SMC iteration (smcdet_mh_sweep_step)."""
+    _fields_ = [("temperature_prev", c_p), ("log_weights_unnorm", c_p), ("weights", c_p),
+                ("ess", c_p), ("log_norm_const", c_p), ("ess_threshold", c_d),
+                ("resample_method", c_i), ("flags", c_u32), ("seed", c_u64), ("offset", c_u64),
+                ("idx", c_p), ("resample_u", c_p), ("finished_iter", c_p), ("live", c_p),
+                ("live_host", c_p), ("iter", c_i), ("reserved", c_i)]
+
+
 _SIGS = {
     "smcdet_version": ([], ctypes.c_char_p),
     "smcdet_abi_version": ([], c_i),
@@ -101,6 +111,10 @@ _SIGS = {
     "smcdet_mh_sweep": ([c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p,
                          c_p, c_p, c_p, c_u64, c_u64, c_p, c_u32, c_p, c_p, c_p, c_p, c_p, c_p],
                         c_i),
+    "smcdet_mh_sweep_step": ([c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p,
+                              c_p, c_p, c_p, c_p, c_u64, c_u64, c_p, c_u32, c_p, c_p, c_p, c_p,
+                              c_p, c_p, c_p], c_i),
+    "smcdet_mh_sweep_step_fused": ([c_p, c_i, c_i, c_u32], c_i),
     "smcdet_mala_sweep": ([c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p,
                            c_p, c_p, c_p, c_u64, c_u64, c_p, c_u32, c_p, c_p, c_p, c_p, c_p],
                           c_i),
@@ -134,8 +148,8 @@ SOURCES = tuple(os.path.join(_REPO, p) for p in (
     "smcdet_amd/csrc/common.hip", "smcdet_amd/csrc/model_kernels.hip",
     "smcdet_amd/csrc/mh_kernel.hip", "smcdet_amd/csrc/mala_kernel.hip",
     "smcdet_amd/csrc/chain_kernel.hip", "smcdet_amd/csrc/smc_kernels.hip",
-    "smcdet_amd/csrc/agg_kernel.hip", "smcdet_amd/csrc/device.h", "smcdet_amd/csrc/render.h", "smcdet_amd/csrc/mcmc.h",
-    "include/smcdet_hip.h"))
+    "smcdet_amd/csrc/agg_kernel.hip", "smcdet_amd/csrc/device.h", "smcdet_amd/csrc/render.h",
+    "smcdet_amd/csrc/mcmc.h", "smcdet_amd/csrc/tile.h", "include/smcdet_hip.h"))
 
 
 def source_hash():

@@ -37,6 +37,7 @@
 #include <type_traits>
 
 #include "render.h"
+#include "tile.h"
 
 namespace smcdet {
 
@@ -81,7 +82,20 @@ struct MhArgs {
   const float* r_uloc;
   const float* r_uflux;
   const float* r_uacc;
+  // fused SMC iteration: the tile's last workgroup runs temper -> reweight ->
+  // next resampling indices (tile.h) on loglik_out right after the sweep
+  int has_tail;
+  TileArgs tail;
 };
+
+// The fused tail: tile_work by the 256 threads of the tile's last workgroup
+// on the 512-thread virtual layout, so the results equal
+// smcdet_temper_reweight's bit for bit.  One instantiation (8 log-likelihoods
+// per virtual thread, N <= 4096, host-checked): smaller N only masks slots,
+// and a masked slot adds an exact 0 to every sum.  Inlined -- as a call, the
+// callee-saved register convention pushed the sweep to 128 VGPRs and
+// scratch.
+constexpr int kTailMaxN = 8 * kTB;
 
 // truncated-normal cache at mean mu: Phi(lb) and log Z, Z = Phi(ub) - Phi(lb)
 // (distributions.py:33-35)
@@ -215,6 +229,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   constexpr int NSL = mh_slots<PPL>();
   extern __shared__ float smem[];
   __shared__ int wg_acc, wg_done;  // last-iteration accepts / finished waves of this workgroup
+  __shared__ int wg_last;          // this workgroup finished its tile last (fused tail)
   if (a.go && *a.go == 0) return;  // speculatively enqueued sweep that must not run
   const DevModel& m = a.m;
   [[maybe_unused]] const int trow = (int)(blockIdx.x * kMhWaves + (threadIdx.x >> 6));
@@ -233,6 +248,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   if (threadIdx.x == 0) {
     wg_acc = 0;
     wg_done = 0;
+    wg_last = 0;
   }
   if (threadIdx.x < kWave) {
     xs[HW + threadIdx.x] = m.bg;
@@ -241,7 +257,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   __syncthreads();
   SMC_TRACE(trow, 1);
   const int n = blockIdx.x * kMhWaves + wave;
-  if (n >= a.N) return;
+  if (n >= a.N) return;  // (never with the fused tail: N % 4 == 0, host-checked)
 
   const int N = a.N, S = a.S;
   const size_t pid = (size_t)t * N + n;
@@ -729,6 +745,24 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
         const int total = atomicExch(cnt, 0);
         atomicExch(ticket, 0);
         a.acc_rate[t] = (float)total / (float)N;
+        wg_last = 1;
+      }
+    }
+  }
+  // ---- fused SMC iteration: the tile's last workgroup tempers, reweights and
+  // draws the next resampling indices once every particle's log-likelihood is
+  // in (the ticket above); its LDS (rate images written back) becomes the
+  // tile pass's buffer.  Not for 8x8 tiles: their 7 workgroups per CU cannot
+  // hold the 2N+1-word buffer (the host launches the tile kernel instead).
+  if constexpr (PPL != 1 && !FULL && PAIRED) {
+    if (a.has_tail) {
+      __shared__ TileRed tail_red;
+      __syncthreads();
+      if (wg_last) {
+        // acquire: the other workgroups' loglik_out stores (released by their
+        // device-scope fence before the ticket)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        tile_work<kMhBlock, 8>(a.tail, t, smem, tail_red, -1);
       }
     }
   }
@@ -780,16 +814,33 @@ using namespace smcdet;
 SMCDET_TRACE_READER(smcdet_trace_read_mh)
 SMCDET_WAVE_READER(smcdet_trace_read_waves)
 
-extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_prior_t* prior,
-                               const smcdet_mh_t* mh, const float* tiled_image,
-                               const float* temperature, int32_t T, int32_t N, int32_t S,
-                               const int64_t* ancestors, const float* counts_in,
-                               const float* locs_in, const float* fluxes_in, float* counts_out,
-                               float* locs_out, float* fluxes_out, const float* rate_in,
-                               float* rate_out, uint64_t seed,
-                               uint64_t offset, const smcdet_mh_replay_t* replay, uint32_t flags,
-                               float* loglik_out, float* acc_rate, int32_t* acc_count,
-                               const int32_t* go, const float* tile_boxes, void* stream) {
+// the fused step's shape test; lds: the launch's dynamic LDS bytes
+static bool tail_fusable(const smcdet_image_model_t& m, int N, int S, uint32_t flags,
+                         size_t* lds) {
+  const size_t HWp = (size_t)m.H * m.W + kWave;
+  const size_t mh_lds =
+      ((m.model == SMCDET_MODEL_POISSON ? 2 : 1) * HWp + (size_t)kMhWaves * HWp) * sizeof(float);
+  const size_t need = mh_lds > tile_lds_bytes(N) ? mh_lds : tile_lds_bytes(N);
+  if (lds) *lds = need;
+  if (flags & (SMCDET_MH_FULL_RECOMPUTE | SMCDET_MH_SCALAR_SLOTS)) return false;
+  if (N % kMhWaves != 0 || N > kTailMaxN) return false;
+  if (S <= kWave && m.H * m.W <= 64) return false;  // small-tile instantiation (PPL = 1)
+  // 4 waves per SIMD = 4 workgroups per CU must still fit the 160 KiB LDS
+  return 4 * (need + 2048) <= 160 * 1024;
+}
+
+static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t* prior,
+                         const smcdet_mh_t* mh, const float* tiled_image,
+                         const float* temperature, int32_t T, int32_t N, int32_t S,
+                         const int64_t* ancestors, const float* counts_in,
+                         const float* locs_in, const float* fluxes_in, float* counts_out,
+                         float* locs_out, float* fluxes_out, const float* rate_in,
+                         float* rate_out, uint64_t seed,
+                         uint64_t offset, const smcdet_mh_replay_t* replay, uint32_t flags,
+                         float* loglik_out, float* acc_rate, int32_t* acc_count,
+                         const int32_t* go, const float* tile_boxes,
+                         const smcdet_smc_tail_t* tail, void* stream) {
+
   int rc = validate_model(model);
   if (rc) return rc;
   rc = validate_prior(prior);
@@ -855,10 +906,53 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
   }
   hipStream_t st = (hipStream_t)stream;
   const size_t HWp = (size_t)model->H * model->W + kWave;
-  const size_t lds =
+  size_t lds =
       ((model->model == SMCDET_MODEL_POISSON ? 2 : 1) * HWp + (size_t)kMhWaves * HWp) *
       sizeof(float);
   const dim3 grid((N + kMhWaves - 1) / kMhWaves, T);
+  bool split_tail = false;  // the tile pass as its own launch(es) after the sweep
+  if (tail) {
+    if (!loglik_out) return set_error(SMCDET_EINVAL, "the fused step needs loglik_out");
+    if (!tail->temperature_prev || !tail->log_weights_unnorm || !tail->weights || !tail->ess ||
+        !tail->log_norm_const)
+      return set_error(SMCDET_EINVAL, "null tail buffer");
+    if (tail->idx && tail->resample_method != SMCDET_RESAMPLE_MULTINOMIAL &&
+        tail->resample_method != SMCDET_RESAMPLE_SYSTEMATIC)
+      return set_error(SMCDET_EINVAL, "unknown resample method %d", tail->resample_method);
+    if (tail->resample_u && tail->resample_method != SMCDET_RESAMPLE_SYSTEMATIC)
+      return set_error(SMCDET_EINVAL, "resample_u replays systematic resampling only");
+    size_t lds_f = 0;
+    if (tail_fusable(*model, N, S, flags, &lds_f)) {
+      TileArgs& ta = a.tail;
+      ta.flags = kDoTemper | kDoWeights | (tail->idx ? kDoResample : 0u);
+      ta.T = T;
+      ta.N = N;
+      ta.ess_threshold = tail->ess_threshold;
+      ta.loglik = loglik_out;
+      ta.temperature = const_cast<float*>(temperature);
+      ta.temperature_prev = tail->temperature_prev;
+      ta.log_w = tail->log_weights_unnorm;
+      ta.weights = tail->weights;
+      ta.ess = tail->ess;
+      ta.logZ = tail->log_norm_const;
+      ta.method = tail->resample_method;
+      ta.k0 = (uint32_t)tail->seed;
+      ta.k1 = (uint32_t)(tail->seed >> 32);
+      ta.offset = tail->offset;
+      ta.u = tail->resample_u;
+      ta.idx = tail->idx;
+      ta.smc_flags = tail->flags;
+      ta.fin_iter = tail->finished_iter;
+      ta.iter = tail->iter;
+      ta.live = tail->live;
+      ta.go = nullptr;  // the sweep already returned when *go == 0
+      ta.live_host = tail->live ? tail->live_host : nullptr;
+      a.has_tail = 1;
+      lds = lds_f;
+    } else {
+      split_tail = true;
+    }
+  }
   const bool full = (flags & SMCDET_MH_FULL_RECOMPUTE) != 0;
   a.ablate = flags & (SMCDET_MH_ABLATE_LIKELIHOOD | SMCDET_MH_ABLATE_PROPOSAL);
   a.by_count = (flags & SMCDET_MH_COMPONENT_BY_COUNT) != 0;
@@ -868,5 +962,64 @@ extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_p
            ? launch_mh<SMCDET_MODEL_M71>(a, replay != nullptr, full, grid, lds, st)
            : launch_mh<SMCDET_MODEL_POISSON>(a, replay != nullptr, full, grid, lds, st);
   if (rc) return rc;
-  return check_launch("smcdet_mh_sweep");
+  rc = check_launch("smcdet_mh_sweep");
+  if (rc || !split_tail) return rc;
+  float* temp = const_cast<float*>(temperature);
+  if (tail->resample_u && tail->idx) {
+    rc = smcdet_temper_reweight(loglik_out, temp, tail->temperature_prev,
+                                tail->log_weights_unnorm, tail->weights, tail->ess,
+                                tail->log_norm_const, T, N, tail->ess_threshold,
+                                tail->resample_method, tail->seed, tail->offset, nullptr,
+                                tail->flags, tail->finished_iter, tail->iter, tail->live, go,
+                                tail->live_host, stream);
+    if (rc) return rc;
+    return smcdet_resample_index(tail->weights, T, N, tail->resample_method, tail->seed,
+                                 tail->offset, tail->resample_u, tail->idx, stream);
+  }
+  return smcdet_temper_reweight(loglik_out, temp, tail->temperature_prev, tail->log_weights_unnorm,
+                                tail->weights, tail->ess, tail->log_norm_const, T, N,
+                                tail->ess_threshold, tail->resample_method, tail->seed,
+                                tail->offset, tail->idx, tail->flags, tail->finished_iter,
+                                tail->iter, tail->live, go, tail->live_host, stream);
+}
+
+extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_prior_t* prior,
+                               const smcdet_mh_t* mh, const float* tiled_image,
+                               const float* temperature, int32_t T, int32_t N, int32_t S,
+                               const int64_t* ancestors, const float* counts_in,
+                               const float* locs_in, const float* fluxes_in, float* counts_out,
+                               float* locs_out, float* fluxes_out, const float* rate_in,
+                               float* rate_out, uint64_t seed,
+                               uint64_t offset, const smcdet_mh_replay_t* replay, uint32_t flags,
+                               float* loglik_out, float* acc_rate, int32_t* acc_count,
+                               const int32_t* go, const float* tile_boxes, void* stream) {
+  return mh_sweep_impl(model, prior, mh, tiled_image, temperature, T, N, S, ancestors, counts_in,
+                       locs_in, fluxes_in, counts_out, locs_out, fluxes_out, rate_in, rate_out,
+                       seed, offset, replay, flags, loglik_out, acc_rate, acc_count, go,
+                       tile_boxes, nullptr, stream);
+}
+
+extern "C" int smcdet_mh_sweep_step(const smcdet_image_model_t* model,
+                                    const smcdet_prior_t* prior, const smcdet_mh_t* mh,
+                                    const float* tiled_image, float* temperature, int32_t T,
+                                    int32_t N, int32_t S, const int64_t* ancestors,
+                                    const float* counts_in, const float* locs_in,
+                                    const float* fluxes_in, float* counts_out, float* locs_out,
+                                    float* fluxes_out, const float* rate_in, float* rate_out,
+                                    uint64_t seed, uint64_t offset,
+                                    const smcdet_mh_replay_t* replay, uint32_t flags,
+                                    float* loglik_out, float* acc_rate, int32_t* acc_count,
+                                    const int32_t* go, const float* tile_boxes,
+                                    const smcdet_smc_tail_t* tail, void* stream) {
+  if (!tail) return set_error(SMCDET_EINVAL, "tail is null");
+  return mh_sweep_impl(model, prior, mh, tiled_image, temperature, T, N, S, ancestors, counts_in,
+                       locs_in, fluxes_in, counts_out, locs_out, fluxes_out, rate_in, rate_out,
+                       seed, offset, replay, flags, loglik_out, acc_rate, acc_count, go,
+                       tile_boxes, tail, stream);
+}
+
+extern "C" int smcdet_mh_sweep_step_fused(const smcdet_image_model_t* model, int32_t N, int32_t S,
+                                          uint32_t flags) {
+  if (!model) return 0;
+  return tail_fusable(*model, N, S, flags, nullptr) ? 1 : 0;
 }

@@ -1,549 +1,25 @@
-// smc_kernels.hip — per-tile SMC bookkeeping on device: adaptive tempering
-// (sampler.py:93-125), reweighting / log-evidence / ESS (sampler.py:181-196),
-// systematic and multinomial resampling (sampler.py:127-169) and pruning
-// (sampler.py:198-219).
-//
-// One 512-thread workgroup per tile does temper -> reweight -> resample
-// indices in one launch, so an SMC iteration needs no host round trip (the
+// smc_kernels.hip — per-tile SMC bookkeeping launches: temper / reweight /
+// resample index (tile.h's tile_work, one 512-thread workgroup per tile; the
 // reference copies the log-likelihoods to the host and runs scipy brentq per
-// tile).  ESS(delta) is monotone, but brentq stops within xtol = 1e-6 of the
-// root, which early in a run is as large as delta itself: the tempering
-// schedule (and so the iteration count) is brentq's, not the exact root's.
-// The root is therefore found by the same Brent iteration as scipy's brentq,
-// each f evaluation being a workgroup-wide reduction.
+// tile), gather, pruning (sampler.py:198-219), the CS-SMC count posterior and
+// the aggregation temper / reweight kernels.
 #include <math.h>
 
-#include "device.h"
+#include "tile.h"
 
 namespace smcdet {
 
 SMCDET_TRACE_TABLE
 
-constexpr int kTB = 512;            // threads per tile workgroup
-constexpr int kTW = kTB / kWave;    // 8 waves (2 per SIMD)
-constexpr int kMaxPer = 32;         // log-likelihoods per thread held in registers
-constexpr int kMaxN = kTB * kMaxPer;
-
-enum : uint32_t { kDoTemper = 1u, kDoWeights = 2u, kDoResample = 4u };
-
-struct TileArgs {
-  uint32_t flags;
-  int T, N;
-  double ess_threshold;
-  const float* loglik;       // [T,N]
-  float* temperature;        // [T]
-  float* temperature_prev;   // [T]
-  float* log_w;              // [T,N]
-  float* weights;            // [T,N]
-  float* ess;                // [T]
-  float* logZ;               // [T]
-  int method;                // SMCDET_RESAMPLE_*
-  uint32_t k0, k1;
-  uint64_t offset;
-  const float* u;            // replay uniforms or null
-  int64_t* idx;              // [T,N]
-  uint32_t smc_flags;        // SMCDET_SMC_*
-  int32_t* fin_iter;         // [T] SMC iteration a tile reached temperature 1 (-1: not yet) or null
-  int32_t iter;              // the caller's SMC iteration number
-  int32_t* live;             // [3] zeroed workspace: counter, ticket, tiles still below 1 (or null)
-  const int32_t* go;         // predicate: skip the launch when *go == 0 (or null)
-  int32_t* live_host;        // host-mapped copy of live[2] (pinned host memory) or null
-};
-
-// end-of-temper bookkeeping, thread 0 of each tile: the iteration at which the
-// tile reached temperature 1, and (last tile, by ticket) the number of tiles
-// still below 1 -- the reference's while condition (sampler.py:230) without
-// extra launches; the counter and ticket are zero again afterwards
-__device__ __forceinline__ void tile_status(const TileArgs& a, int t, float tnew) {
-  if (a.fin_iter && tnew >= 1.0f && a.fin_iter[t] < 0) a.fin_iter[t] = a.iter;
-  if (a.live) {
-    atomicAdd(&a.live[0], tnew < 1.0f ? 1 : 0);
-    __threadfence();
-    if (atomicAdd(&a.live[1], 1) == a.T - 1) {
-      const int nlive = atomicExch(&a.live[0], 0);
-      a.live[2] = nlive;
-      atomicExch(&a.live[1], 0);
-      if (a.live_host) {  // the host reads it after the launch completes: no copy launch
-        *reinterpret_cast<volatile int32_t*>(a.live_host) = nlive;
-        __threadfence_system();
-      }
-    }
-  }
-}
-
-// Workgroup reductions with ONE barrier each: wave DPP reductions -> per-wave
-// slots of a double-buffered LDS array -> every thread combines the kTW slots
-// in a fixed order (deterministic; every thread ends with the same value).
-// `parity` lives in registers and toggles identically in every thread, so a
-// buffer is not rewritten before all threads passed the next call's barrier.
-struct TileRed {
-  double d[2][kTW][2];
-  float f[2][kTW];
-  float f2[2][kTW][2];
-  int i[2][kTW];
-};
-__device__ __forceinline__ void block_sum2(double& a, double& b, TileRed* r, int& parity) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  a = wave_sum(a);
-  b = wave_sum(b);
-  const int k = parity;
-  parity ^= 1;
-  if (lane == 0) {
-    r->d[k][wave][0] = a;
-    r->d[k][wave][1] = b;
-  }
-  __syncthreads();
-  double sa = 0.0, sb = 0.0;
-#pragma unroll
-  for (int i = 0; i < kTW; ++i) {
-    sa += r->d[k][i][0];
-    sb += r->d[k][i][1];
-  }
-  a = sa;
-  b = sb;
-}
-__device__ __forceinline__ void block_sum2f(float& a, float& b, TileRed* r, int& parity) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  a = wave_sum(a);
-  b = wave_sum(b);
-  const int k = parity;
-  parity ^= 1;
-  if (lane == 0) {
-    r->f2[k][wave][0] = a;
-    r->f2[k][wave][1] = b;
-  }
-  __syncthreads();
-  float sa[kTW], sb[kTW];
-#pragma unroll
-  for (int i = 0; i < kTW; ++i) {
-    sa[i] = r->f2[k][i][0];
-    sb[i] = r->f2[k][i][1];
-  }
-#pragma unroll
-  for (int w = 1; w < kTW; w <<= 1) {
-#pragma unroll
-    for (int i = 0; i + w < kTW; i += 2 * w) {
-      sa[i] += sa[i + w];
-      sb[i] += sb[i + w];
-    }
-  }
-  a = sa[0];
-  b = sb[0];
-}
-__device__ __forceinline__ float block_max(float v, TileRed* r, int& parity) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  v = wave_max(v);
-  const int k = parity;
-  parity ^= 1;
-  if (lane == 0) r->f[k][wave] = v;
-  __syncthreads();
-  float m = -INFINITY;
-#pragma unroll
-  for (int i = 0; i < kTW; ++i) m = fmaxf(m, r->f[k][i]);
-  return m;
-}
-
-// Pairwise (depth log2 PER) sum of a register array: short dependency chains,
-// which is what a one-workgroup-per-tile kernel with nothing to hide latency
-// behind needs.
-template <class V, int PER>
-__device__ __forceinline__ V tree_sum(V (&x)[PER]) {
-#pragma unroll
-  for (int w = 1; w < PER; w <<= 1) {
-#pragma unroll
-    for (int j = 0; j + w < PER; j += 2 * w) x[j] += x[j + w];
-  }
-  return x[0];
-}
-
-// a / b by v_rcp_f64 + two Newton steps + one residual correction: the
-// quotient to the last bit or so, without the IEEE division sequence's scale /
-// fixup steps on the latency-bound Brent path (b = 0 or inf gives a NaN/inf
-// step, which the Brent tests reject exactly as they reject scipy's)
-__device__ __forceinline__ double ddiv(double a, double b) {
-  double r = __builtin_amdgcn_rcp(b);
-  r = fma(fma(-b, r, 1.0), r, r);
-  r = fma(fma(-b, r, 1.0), r, r);
-  const double q = a * r;
-  return fma(fma(-b, q, a), r, q);
-}
-
-// Each thread's log-likelihoods (i = threadIdx.x + j*kTB) live in registers
-// for the whole tempering search.
-template <int PER>
-struct TileLL {
-  float l[PER];
-  __device__ __forceinline__ bool valid(int j, int N) const {
-    return (int)threadIdx.x + j * kTB < N;
-  }
-};
-
-// f(delta) = ESS(delta) - threshold: ESS = (sum e)^2 / sum e^2,
-// e = exp(d*l - max(d*l)), d = float32(delta) (the reference multiplies its
-// float32 log-likelihoods by the python float delta and reduces in float32;
-// sampler.py:93-97).  Sums are float32 pairwise trees (relative error ~1e-6,
-// the reference's own float32 logsumexp level); only the ratio is double.
-// This sits on the latency-bound path of every Brent iteration, so it is
-// short: one exp per element, float DPP reductions, one barrier.
-template <int PER>
-__device__ __forceinline__ double block_ess_objective(const TileLL<PER>& ll, int N, float lmax,
-                                                      double delta, double thr, TileRed* red,
-                                                      int& parity) {
-  const float df = (float)delta;
-  const float m = df * lmax;  // = max_i fl(df*l_i): rounding is monotone
-  float e1[PER], e2[PER];
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const float e = ll.valid(j, N) ? fast_exp2((df * ll.l[j] - m) * kLog2e) : 0.f;
-    e1[j] = e;
-    e2[j] = e * e;
-  }
-  float s1 = tree_sum(e1), s2 = tree_sum(e2);
-  block_sum2f(s1, s2, red, parity);
-  const double d1 = (double)s1;
-  return ddiv(d1 * d1, (double)s2) - thr;
-}
-
-// scipy.optimize.brentq (scipy/optimize/Zeros/brentq.c, the algorithm the
-// reference calls at sampler.py:114-120) with xtol = rtol = 1e-6, maxiter
-// 100.  Every thread runs the (deterministic) control flow on identical
-// values; the workgroup evaluates f together.
-template <class F>
-__device__ double block_brentq(F&& f, double xa, double xb, double fa, double fb) {
-  const double xtol = 1e-6, rtol = 1e-6;
-  double xpre = xa, xcur = xb, xblk = 0., fpre = fa, fcur = fb, fblk = 0., spre = 0., scur = 0.;
-  if (fpre == 0.0) return xpre;
-  if (fcur == 0.0) return xcur;
-  for (int it = 0; it < 100; ++it) {
-    if (fpre != 0 && fcur != 0 && (signbit(fpre) != signbit(fcur))) {
-      xblk = xpre;
-      fblk = fpre;
-      spre = scur = xcur - xpre;
-    }
-    if (fabs(fblk) < fabs(fcur)) {
-      xpre = xcur; xcur = xblk; xblk = xpre;
-      fpre = fcur; fcur = fblk; fblk = fpre;
-    }
-    const double delta = (xtol + rtol * fabs(xcur)) / 2;
-    const double sbis = (xblk - xcur) / 2;
-    if (fcur == 0 || fabs(sbis) < delta) return xcur;
-    if (fabs(spre) > delta && fabs(fcur) < fabs(fpre)) {
-      double stry;
-      if (xpre == xblk) {
-        stry = ddiv(-fcur * (xcur - xpre), fcur - fpre);  // interpolate
-      } else {                                         // extrapolate
-        const double dpre = ddiv(fpre - fcur, xpre - xcur);
-        const double dblk = ddiv(fblk - fcur, xblk - xcur);
-        stry = ddiv(-fcur * (fblk * dblk - fpre * dpre), dblk * dpre * (fblk - fpre));
-      }
-      if (2 * fabs(stry) < fmin(fabs(spre), 3 * fabs(sbis) - delta)) {
-        spre = scur;
-        scur = stry;
-      } else {
-        spre = sbis;
-        scur = sbis;
-      }
-    } else {
-      spre = sbis;
-      scur = sbis;
-    }
-    xpre = xcur;
-    fpre = fcur;
-    if (fabs(scur) > delta) xcur += scur;
-    else xcur += (sbis > 0 ? delta : -delta);
-    fcur = f(xcur);
-  }
-  return xcur;
-}
-
+// One 512-thread workgroup per tile (tile.h: the same work the MH sweep's
+// last workgroup runs when the SMC iteration is fused into one launch).
 template <int PER>
 __global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
   if (a.go && *a.go == 0) return;  // speculatively enqueued iteration that must not run
   extern __shared__ float buf[];  // N floats: weights / cumsum, then N+1 resample slots
   __shared__ TileRed red;
-  int parity = 0;
   const int t = blockIdx.x;
-  const int N = a.N;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-
-  [[maybe_unused]] const int trow = threadIdx.x < kWave ? t : -1;
-  SMC_TRACE(trow, 0);
-  // independent stopping: a finished tile stays as it is (uniform weights of
-  // its final resampled population, identity ancestors, log Z unchanged)
-  if ((a.smc_flags & SMCDET_SMC_FREEZE_DONE) && a.temperature[t] >= 1.0f) {
-    if ((a.flags & kDoTemper) && threadIdx.x == 0) {
-      a.temperature_prev[t] = a.temperature[t];
-      tile_status(a, t, a.temperature[t]);
-    }
-    if (a.flags & kDoWeights) {
-      for (int i = threadIdx.x; i < N; i += kTB) {
-        a.log_w[(size_t)t * N + i] = 0.0f;
-        a.weights[(size_t)t * N + i] = 1.0f / (float)N;
-      }
-      // a.ess[t] keeps the ESS of the tile's last step, as a single-tile
-      // run of the reference reports it after its final resample
-    }
-    if (a.flags & kDoResample)
-      for (int i = threadIdx.x; i < N; i += kTB) a.idx[(size_t)t * N + i] = i;
-    return;
-  }
-  TileLL<PER> ll;
-  if (a.flags & (kDoTemper | kDoWeights)) {
-    const float* llg = a.loglik + (size_t)t * N;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) ll.l[j] = ll.valid(j, N) ? llg[threadIdx.x + j * kTB] : 0.f;
-  }
-
-  // ------------------------------------------------------------------ temper
-  float d_new = 0.f;  // float32 temperature increment, when tempered here
-  if (a.flags & kDoTemper) {
-    const float tau = a.temperature[t];
-    float lm = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < PER; ++j)
-      if (ll.valid(j, N)) lm = fmaxf(lm, ll.l[j]);
-    lm = block_max(lm, &red, parity);
-    SMC_TRACE(trow, 1);
-    const double thr = a.ess_threshold;
-    auto f = [&](double x) { return block_ess_objective(ll, N, lm, x, thr, &red, parity); };
-    const double top = 1.0 - (double)tau;
-    // sampler.py:113-122: root-find only if ESS at delta = 1 - tau is below threshold
-    const double ftop = f(top);
-    SMC_TRACE(trow, 2);
-    double delta = top;
-    // f(0) = N - thr exactly: every weight is exp(0) = 1
-    if (ftop < 0.0) delta = block_brentq(f, 0.0, top, (double)N - thr, ftop);
-    SMC_TRACE(trow, 3);
-    const float tnew = tau + (float)delta;  // delta tensor is float32 (sampler.py:105)
-    d_new = tnew - tau;
-    if (threadIdx.x == 0) {
-      a.temperature_prev[t] = tau;
-      a.temperature[t] = tnew;
-      tile_status(a, t, tnew);
-    }
-  }
-
-  // ------------------------------------------------------------ update weights
-  if (a.flags & kDoWeights) {
-    const float d = (a.flags & kDoTemper) ? d_new : a.temperature[t] - a.temperature_prev[t];
-    float* lwg = a.log_w + (size_t)t * N;
-    float* wg = a.weights + (size_t)t * N;
-    float e[PER];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      e[j] = nan_to_num(d * ll.l[j], -INFINITY);
-      if (ll.valid(j, N)) {
-        lwg[threadIdx.x + j * kTB] = e[j];
-        mx = fmaxf(mx, e[j]);
-      }
-    }
-    mx = block_max(mx, &red, parity);
-    double s[PER];
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      e[j] = ll.valid(j, N) ? expf(e[j] - mx) : 0.f;
-      s[j] = (double)e[j];
-    }
-    double ssum = tree_sum(s), unused = 0.0;
-    block_sum2(ssum, unused, &red, parity);
-    const float sf = (float)ssum;
-    double q[PER];
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const float wv = e[j] / sf;
-      q[j] = (double)wv * (double)wv;
-      if (ll.valid(j, N)) {
-        wg[threadIdx.x + j * kTB] = wv;
-        buf[threadIdx.x + j * kTB] = wv;
-      }
-    }
-    double qs = tree_sum(q);
-    block_sum2(qs, unused, &red, parity);
-    SMC_TRACE(trow, 4);
-    if (threadIdx.x == 0) {
-      a.ess[t] = (float)(1.0 / qs);
-      a.logZ[t] = (a.logZ[t] + mx) + logf(sf / (float)N);
-    }
-  }
-
-  // ---------------------------------------------------------- resample index
-  if (a.flags & kDoResample) {
-    if (!(a.flags & kDoWeights)) {
-      const float* W = a.weights + (size_t)t * N;
-      for (int i = threadIdx.x; i < N; i += kTB) buf[i] = W[i];
-    }
-    __syncthreads();
-    // bins = cumsum(W): float64 running sum rounded per element to float32
-    // (what torch's CPU cumsum does), contiguous chunk per thread, in place
-    const int chunk = (N + kTB - 1) / kTB;
-    const int b0 = min((int)threadIdx.x * chunk, N), b1 = min(b0 + chunk, N);
-    // chunks of 8 (N = 4096) move as two 16-byte LDS accesses per thread
-    const bool vec8 = chunk == 8 && (N & 7) == 0;
-    float cv[8];
-    double part = 0.0;
-    if (vec8) {
-      if (b0 < b1) {
-        const float4 v0 = *reinterpret_cast<const float4*>(buf + b0);
-        const float4 v1 = *reinterpret_cast<const float4*>(buf + b0 + 4);
-        cv[0] = v0.x; cv[1] = v0.y; cv[2] = v0.z; cv[3] = v0.w;
-        cv[4] = v1.x; cv[5] = v1.y; cv[6] = v1.z; cv[7] = v1.w;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) part += (double)cv[i];
-      }
-    } else {
-      for (int i = b0; i < b1; ++i) part += (double)buf[i];
-    }
-    double incl = part;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const double y = __shfl_up(incl, o, kWave);
-      if (lane >= o) incl += y;
-    }
-    const int k = parity;
-    parity ^= 1;
-    if (lane == 63) red.d[k][wave][0] = incl;
-    __syncthreads();
-    SMC_TRACE(trow, 5);
-    double base = 0.0;
-    for (int i = 0; i < wave; ++i) base += red.d[k][i][0];
-    double run = base + incl - part;
-    if (vec8) {
-      if (b0 < b1) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          run += (double)cv[i];
-          cv[i] = (float)run;
-        }
-        *reinterpret_cast<float4*>(buf + b0) = make_float4(cv[0], cv[1], cv[2], cv[3]);
-        *reinterpret_cast<float4*>(buf + b0 + 4) = make_float4(cv[4], cv[5], cv[6], cv[7]);
-      }
-    } else {
-      for (int i = b0; i < b1; ++i) {
-        run += (double)buf[i];
-        buf[i] = (float)run;
-      }
-    }
-    __syncthreads();
-    float U = 0.f;
-    if (a.method == SMCDET_RESAMPLE_SYSTEMATIC) {
-      if (a.u) {
-        U = a.u[t];
-      } else {
-        const U4 r = philox4x32((uint32_t)a.offset, (uint32_t)(a.offset >> 32), (uint32_t)t,
-                                kTagResample, a.k0, a.k1);
-        U = u01(r.x);
-      }
-    }
-    const float total = buf[N - 1];
-    int64_t* idxg = a.idx + (size_t)t * N;
-    if (a.method == SMCDET_RESAMPLE_SYSTEMATIC) {
-      // bucketize(u, bins), u_n = (n + U) / N in float32 (sampler.py:144),
-      // right=False: idx[n] = #{i : bins[i] < u_n}.  With cnt(i) = #{n : u_n <= bins[i]}
-      // (monotone in i), idx[n] = #{i : cnt(i) <= n}: the last bin of every run of
-      // equal cnt writes i+1 to slot[cnt], and a prefix max over slots gives idx.
-      // Exact (u_n is recomputed with the same float ops) and load-balanced
-      // whatever the weight degeneracy, unlike a per-n search.
-      int* slot = reinterpret_cast<int*>(buf + N);  // N+1 ints
-      const float Nf = (float)N;
-      auto un = [&](int n) { return ((float)n + U) / Nf; };
-      // For N a power of two the division is an exact scaling:
-      // u_n <= b  <=>  fl(n + U) <= b*N (exact), and n <= fl(n + U) <= n + 1,
-      // so every n < floor(b*N) counts and only n = floor(b*N) needs a test.
-      const bool pow2 = (N & (N - 1)) == 0;
-      auto cnt = [&](float b) {
-        if (pow2) {
-          const float B = b * Nf;
-          int c = (int)fminf(fmaxf(floorf(B), 0.f), Nf);
-          c += (c < N && (float)c + U <= B) ? 1 : 0;
-          return c;
-        }
-        int c = (int)fminf(fmaxf(floorf(b * Nf - U), 0.f), Nf);
-        while (c > 0 && un(c - 1) > b) --c;
-        while (c < N && un(c) <= b) ++c;
-        return c;
-      };
-      for (int i = threadIdx.x; i <= N; i += kTB) slot[i] = 0;
-      __syncthreads();
-      SMC_TRACE(trow, 6);
-      for (int i = threadIdx.x; i < N; i += kTB) {
-        const int ci = cnt(buf[i]);
-        const int cnext = (i + 1 < N) ? cnt(buf[i + 1]) : -1;
-        if (cnext != ci) slot[ci] = i + 1;
-      }
-      __syncthreads();
-      SMC_TRACE(trow, 7);
-      // prefix max over slot[0..N-1], contiguous chunk per thread
-      int pm = 0;
-      int sv[8];
-      if (vec8) {
-        if (b0 < b1) {
-          const int4 v0 = *reinterpret_cast<const int4*>(slot + b0);
-          const int4 v1 = *reinterpret_cast<const int4*>(slot + b0 + 4);
-          sv[0] = v0.x; sv[1] = v0.y; sv[2] = v0.z; sv[3] = v0.w;
-          sv[4] = v1.x; sv[5] = v1.y; sv[6] = v1.z; sv[7] = v1.w;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) pm = max(pm, sv[i]);
-        }
-      } else {
-        for (int i = b0; i < b1; ++i) pm = max(pm, slot[i]);
-      }
-      int incl_m = pm;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl_m, o, kWave);
-        if (lane >= o) incl_m = max(incl_m, y);
-      }
-      const int k2 = parity;
-      parity ^= 1;
-      if (lane == 63) red.i[k2][wave] = incl_m;
-      __syncthreads();
-      int run_m = __shfl_up(incl_m, 1, kWave);
-      if (lane == 0) run_m = 0;
-      for (int i = 0; i < wave; ++i) run_m = max(run_m, red.i[k2][i]);
-      // in place: slot[i] becomes idx[i] (each thread owns its chunk)
-      if (vec8) {
-        if (b0 < b1) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            run_m = max(run_m, sv[i]);
-            sv[i] = min(run_m, N - 1);
-          }
-          *reinterpret_cast<int4*>(slot + b0) = make_int4(sv[0], sv[1], sv[2], sv[3]);
-          *reinterpret_cast<int4*>(slot + b0 + 4) = make_int4(sv[4], sv[5], sv[6], sv[7]);
-        }
-      } else {
-        for (int i = b0; i < b1; ++i) {
-          run_m = max(run_m, slot[i]);
-          slot[i] = min(run_m, N - 1);
-        }
-      }
-      __syncthreads();
-      SMC_TRACE(trow, 8);
-      for (int n = threadIdx.x; n < N; n += kTB) idxg[n] = (int64_t)slot[n];
-      SMC_TRACE(trow, 9);
-    } else {
-      // multinomial (sampler.py:127-140): target = u * total, first bin > target
-      for (int n = threadIdx.x; n < N; n += kTB) {
-        float un;
-        if (a.u) {
-          un = a.u[(size_t)t * N + n];
-        } else {
-          const uint64_t c = a.offset + (uint64_t)n;
-          const U4 r = philox4x32((uint32_t)c, (uint32_t)(c >> 32), (uint32_t)t,
-                                  kTagResample + 1, a.k0, a.k1);
-          un = u01(r.x);
-        }
-        const float target = un * total;
-        int lo = 0, hi = N;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (buf[mid] > target) hi = mid; else lo = mid + 1;
-        }
-        idxg[n] = (int64_t)min(lo, N - 1);
-      }
-    }
-  }
+  tile_work<kTB, PER>(a, t, buf, red, threadIdx.x < kWave ? t : -1);
 }
 
 // gather: thread per (t, n, s)
@@ -730,16 +206,16 @@ __global__ __launch_bounds__(kTB) void agg_temper_kernel(AggTileArgs a) {
     return;
   }
   const size_t base = (size_t)t * a.N + s0;
-  TileLL<PER> ll;
+  TileLL<kTB, PER> ll;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int i = threadIdx.x + j * kTB;
-    ll.l[j] = ll.valid(j, n) ? a.ll_parent[base + i] - a.ll_child[base + i] : 0.f;
+    ll.l[0][j] = ll.valid(0, j, n) ? a.ll_parent[base + i] - a.ll_child[base + i] : 0.f;
   }
   float lm = -INFINITY;
 #pragma unroll
   for (int j = 0; j < PER; ++j)
-    if (ll.valid(j, n)) lm = fmaxf(lm, ll.l[j]);
+    if (ll.valid(0, j, n)) lm = fmaxf(lm, ll.l[0][j]);
   lm = block_max(lm, &red, parity);
   const double thr = a.ess_prop * (double)n;
   auto f = [&](double x) { return block_ess_objective(ll, n, lm, x, thr, &red, parity); };

@@ -1,0 +1,644 @@
+// tile.h — per-tile SMC bookkeeping on device: adaptive tempering
+// (sampler.py:93-125), reweighting / log-evidence / ESS (sampler.py:181-196)
+// and the next resampling indices (sampler.py:127-169), as one workgroup's
+// work over one tile's N particles.
+//
+// Two callers: tile_kernel (smc_kernels.hip, one 512-thread workgroup per
+// tile) and the MH sweep's tail (mh_kernel.hip: the tile's last-finishing
+// 256-thread workgroup runs it right after its own particles, so an SMC
+// iteration is one launch).  Both compute on the same *virtual* layout of
+// kTB = 512 threads: a physical thread of an NT-thread workgroup plays the
+// virtual threads tid + h*NT (h < 512/NT), virtual wave `wave + h*NT/64`
+// being physical wave `wave`'s lanes.  Every reduction, scan and Brent step
+// is therefore the same sequence of float operations whichever workgroup
+// runs it: the fused and the separate launch give bit-identical temperatures,
+// weights and indices.
+//
+// ESS(delta) is monotone, but brentq stops within xtol = 1e-6 of the root,
+// which early in a run is as large as delta itself: the tempering schedule
+// (and so the iteration count) is brentq's, not the exact root's.  The root
+// is therefore found by the same Brent iteration as scipy's brentq, each f
+// evaluation being a workgroup-wide reduction.
+#pragma once
+
+#include <math.h>
+
+#include "device.h"
+
+namespace smcdet {
+
+constexpr int kTB = 512;            // virtual threads of the tile layout
+constexpr int kTW = kTB / kWave;    // 8 virtual waves
+constexpr int kMaxPer = 32;         // log-likelihoods per virtual thread
+constexpr int kMaxN = kTB * kMaxPer;
+
+enum : uint32_t { kDoTemper = 1u, kDoWeights = 2u, kDoResample = 4u };
+
+struct TileArgs {
+  uint32_t flags;
+  int T, N;
+  double ess_threshold;
+  const float* loglik;       // [T,N]
+  float* temperature;        // [T]
+  float* temperature_prev;   // [T]
+  float* log_w;              // [T,N]
+  float* weights;            // [T,N]
+  float* ess;                // [T]
+  float* logZ;               // [T]
+  int method;                // SMCDET_RESAMPLE_*
+  uint32_t k0, k1;
+  uint64_t offset;
+  const float* u;            // replay uniforms or null
+  int64_t* idx;              // [T,N]
+  uint32_t smc_flags;        // SMCDET_SMC_*
+  int32_t* fin_iter;         // [T] SMC iteration a tile reached temperature 1 (-1: not yet) or null
+  int32_t iter;              // the caller's SMC iteration number
+  int32_t* live;             // [3] zeroed workspace: counter, ticket, tiles still below 1 (or null)
+  const int32_t* go;         // predicate: skip the launch when *go == 0 (or null)
+  int32_t* live_host;        // host-mapped copy of live[2] (pinned host memory) or null
+};
+
+// end-of-temper bookkeeping, thread 0 of each tile: the iteration at which the
+// tile reached temperature 1, and (last tile, by ticket) the number of tiles
+// still below 1 -- the reference's while condition (sampler.py:230) without
+// extra launches; the counter and ticket are zero again afterwards
+__device__ __forceinline__ void tile_status(const TileArgs& a, int t, float tnew) {
+  if (a.fin_iter && tnew >= 1.0f && a.fin_iter[t] < 0) a.fin_iter[t] = a.iter;
+  if (a.live) {
+    atomicAdd(&a.live[0], tnew < 1.0f ? 1 : 0);
+    __threadfence();
+    if (atomicAdd(&a.live[1], 1) == a.T - 1) {
+      const int nlive = atomicExch(&a.live[0], 0);
+      a.live[2] = nlive;
+      atomicExch(&a.live[1], 0);
+      if (a.live_host) {  // the host reads it after the launch completes: no copy launch
+        *reinterpret_cast<volatile int32_t*>(a.live_host) = nlive;
+        __threadfence_system();
+      }
+    }
+  }
+}
+
+// Per-virtual-wave partials of the workgroup reductions, double-buffered.
+// `parity` lives in registers and toggles identically in every thread, so a
+// buffer is not rewritten before all threads passed the next call's barrier.
+struct TileRed {
+  double d[2][kTW][2];
+  float f[2][kTW];
+  float f2[2][kTW][2];
+  int i[2][kTW];
+};
+
+template <int NT>
+struct VLayout {
+  static_assert(NT % kWave == 0 && kTB % NT == 0, "NT must divide the 512-thread layout");
+  static constexpr int VPT = kTB / NT;  // virtual threads per physical thread
+  static constexpr int NW = NT / kWave;
+};
+template <int NT>
+__device__ __forceinline__ int vthread(int h) {
+  return (int)threadIdx.x + h * NT;
+}
+template <int NT>
+__device__ __forceinline__ int vwave(int h) {
+  return ((int)threadIdx.x >> 6) + h * VLayout<NT>::NW;
+}
+
+// Workgroup reductions with ONE barrier each: wave DPP reductions per virtual
+// wave -> its slot -> every thread combines the kTW slots in a fixed order
+// (deterministic; every thread ends with the same value).
+template <int NT>
+__device__ __forceinline__ double vblock_sumd(const double (&a)[VLayout<NT>::VPT], TileRed* r,
+                                              int& parity) {
+  const int lane = threadIdx.x & 63;
+  const int k = parity;
+  parity ^= 1;
+#pragma unroll
+  for (int h = 0; h < VLayout<NT>::VPT; ++h) {
+    const double s = wave_sum(a[h]);
+    if (lane == 0) r->d[k][vwave<NT>(h)][0] = s;
+  }
+  __syncthreads();
+  double sa = 0.0;
+#pragma unroll
+  for (int i = 0; i < kTW; ++i) sa += r->d[k][i][0];
+  return sa;
+}
+template <int NT>
+__device__ __forceinline__ void vblock_sum2f(const float (&a)[VLayout<NT>::VPT],
+                                             const float (&b)[VLayout<NT>::VPT], float& A,
+                                             float& B, TileRed* r, int& parity) {
+  const int lane = threadIdx.x & 63;
+  const int k = parity;
+  parity ^= 1;
+#pragma unroll
+  for (int h = 0; h < VLayout<NT>::VPT; ++h) {
+    const float x = wave_sum(a[h]), y = wave_sum(b[h]);
+    if (lane == 0) {
+      r->f2[k][vwave<NT>(h)][0] = x;
+      r->f2[k][vwave<NT>(h)][1] = y;
+    }
+  }
+  __syncthreads();
+  float sa[kTW], sb[kTW];
+#pragma unroll
+  for (int i = 0; i < kTW; ++i) {
+    sa[i] = r->f2[k][i][0];
+    sb[i] = r->f2[k][i][1];
+  }
+#pragma unroll
+  for (int w = 1; w < kTW; w <<= 1) {
+#pragma unroll
+    for (int i = 0; i + w < kTW; i += 2 * w) {
+      sa[i] += sa[i + w];
+      sb[i] += sb[i + w];
+    }
+  }
+  A = sa[0];
+  B = sb[0];
+}
+template <int NT>
+__device__ __forceinline__ float vblock_max(const float (&v)[VLayout<NT>::VPT], TileRed* r,
+                                            int& parity) {
+  const int lane = threadIdx.x & 63;
+  const int k = parity;
+  parity ^= 1;
+#pragma unroll
+  for (int h = 0; h < VLayout<NT>::VPT; ++h) {
+    const float m = wave_max(v[h]);
+    if (lane == 0) r->f[k][vwave<NT>(h)] = m;
+  }
+  __syncthreads();
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < kTW; ++i) m = fmaxf(m, r->f[k][i]);
+  return m;
+}
+
+// the 512-thread forms (aggregation kernels)
+__device__ __forceinline__ float block_max(float v, TileRed* r, int& parity) {
+  const float a[1] = {v};
+  return vblock_max<kTB>(a, r, parity);
+}
+__device__ __forceinline__ void block_sum2(double& a, double& /*unused*/, TileRed* r,
+                                           int& parity) {
+  const double x[1] = {a};
+  a = vblock_sumd<kTB>(x, r, parity);
+}
+
+// Pairwise (depth log2 PER) sum of a register array: short dependency chains,
+// which is what a one-workgroup-per-tile pass with nothing to hide latency
+// behind needs.
+template <class V, int PER>
+__device__ __forceinline__ V tree_sum(V (&x)[PER]) {
+#pragma unroll
+  for (int w = 1; w < PER; w <<= 1) {
+#pragma unroll
+    for (int j = 0; j + w < PER; j += 2 * w) x[j] += x[j + w];
+  }
+  return x[0];
+}
+
+// a / b by v_rcp_f64 + two Newton steps + one residual correction: the
+// quotient to the last bit or so, without the IEEE division sequence's scale /
+// fixup steps on the latency-bound Brent path (b = 0 or inf gives a NaN/inf
+// step, which the Brent tests reject exactly as they reject scipy's)
+__device__ __forceinline__ double ddiv(double a, double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  r = fma(fma(-b, r, 1.0), r, r);
+  r = fma(fma(-b, r, 1.0), r, r);
+  const double q = a * r;
+  return fma(fma(-b, q, a), r, q);
+}
+
+// The log-likelihoods of virtual thread v (i = v + j*kTB) live in registers
+// for the whole tempering search.
+template <int NT, int PER>
+struct TileLL {
+  float l[VLayout<NT>::VPT][PER];
+  __device__ __forceinline__ bool valid(int h, int j, int N) const {
+    return vthread<NT>(h) + j * kTB < N;
+  }
+};
+
+// f(delta) = ESS(delta) - threshold: ESS = (sum e)^2 / sum e^2,
+// e = exp(d*l - max(d*l)), d = float32(delta) (the reference multiplies its
+// float32 log-likelihoods by the python float delta and reduces in float32;
+// sampler.py:93-97).  Sums are float32 pairwise trees (relative error ~1e-6,
+// the reference's own float32 logsumexp level); only the ratio is double.
+// This sits on the latency-bound path of every Brent iteration, so it is
+// short: one exp per element, float DPP reductions, one barrier.
+template <int NT, int PER>
+__device__ __forceinline__ double block_ess_objective(const TileLL<NT, PER>& ll, int N, float lmax,
+                                                      double delta, double thr, TileRed* red,
+                                                      int& parity) {
+  constexpr int VPT = VLayout<NT>::VPT;
+  const float df = (float)delta;
+  const float m = df * lmax;  // = max_i fl(df*l_i): rounding is monotone
+  float s1[VPT], s2[VPT];
+#pragma unroll
+  for (int h = 0; h < VPT; ++h) {
+    float e1[PER], e2[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const float e = ll.valid(h, j, N) ? fast_exp2((df * ll.l[h][j] - m) * kLog2e) : 0.f;
+      e1[j] = e;
+      e2[j] = e * e;
+    }
+    s1[h] = tree_sum(e1);
+    s2[h] = tree_sum(e2);
+  }
+  float S1, S2;
+  vblock_sum2f<NT>(s1, s2, S1, S2, red, parity);
+  const double d1 = (double)S1;
+  return ddiv(d1 * d1, (double)S2) - thr;
+}
+
+// scipy.optimize.brentq (scipy/optimize/Zeros/brentq.c, the algorithm the
+// reference calls at sampler.py:114-120) with xtol = rtol = 1e-6, maxiter
+// 100.  Every thread runs the (deterministic) control flow on identical
+// values; the workgroup evaluates f together.
+template <class F>
+__device__ double block_brentq(F&& f, double xa, double xb, double fa, double fb) {
+  const double xtol = 1e-6, rtol = 1e-6;
+  double xpre = xa, xcur = xb, xblk = 0., fpre = fa, fcur = fb, fblk = 0., spre = 0., scur = 0.;
+  if (fpre == 0.0) return xpre;
+  if (fcur == 0.0) return xcur;
+  for (int it = 0; it < 100; ++it) {
+    if (fpre != 0 && fcur != 0 && (signbit(fpre) != signbit(fcur))) {
+      xblk = xpre;
+      fblk = fpre;
+      spre = scur = xcur - xpre;
+    }
+    if (fabs(fblk) < fabs(fcur)) {
+      xpre = xcur; xcur = xblk; xblk = xpre;
+      fpre = fcur; fcur = fblk; fblk = fpre;
+    }
+    const double delta = (xtol + rtol * fabs(xcur)) / 2;
+    const double sbis = (xblk - xcur) / 2;
+    if (fcur == 0 || fabs(sbis) < delta) return xcur;
+    if (fabs(spre) > delta && fabs(fcur) < fabs(fpre)) {
+      double stry;
+      if (xpre == xblk) {
+        stry = ddiv(-fcur * (xcur - xpre), fcur - fpre);  // interpolate
+      } else {                                         // extrapolate
+        const double dpre = ddiv(fpre - fcur, xpre - xcur);
+        const double dblk = ddiv(fblk - fcur, xblk - xcur);
+        stry = ddiv(-fcur * (fblk * dblk - fpre * dpre), dblk * dpre * (fblk - fpre));
+      }
+      if (2 * fabs(stry) < fmin(fabs(spre), 3 * fabs(sbis) - delta)) {
+        spre = scur;
+        scur = stry;
+      } else {
+        spre = sbis;
+        scur = sbis;
+      }
+    } else {
+      spre = sbis;
+      scur = sbis;
+    }
+    xpre = xcur;
+    fpre = fcur;
+    if (fabs(scur) > delta) xcur += scur;
+    else xcur += (sbis > 0 ? delta : -delta);
+    fcur = f(xcur);
+  }
+  return xcur;
+}
+
+// One tile's temper -> reweight -> resample-index pass (a.flags select the
+// parts) by an NT-thread workgroup.  buf: 2N+1 words of LDS (weights /
+// cumsum, then N+1 resampling slots).  trow: SMC_TRACE row (-1: none).
+template <int NT, int PER>
+__device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, TileRed& red,
+                                          [[maybe_unused]] int trow) {
+  constexpr int VPT = VLayout<NT>::VPT;
+  int parity = 0;
+  const int N = a.N;
+  const int lane = threadIdx.x & 63;
+
+  SMC_TRACE(trow, 0);
+  // independent stopping: a finished tile stays as it is (uniform weights of
+  // its final resampled population, identity ancestors, log Z unchanged)
+  if ((a.smc_flags & SMCDET_SMC_FREEZE_DONE) && a.temperature[t] >= 1.0f) {
+    if ((a.flags & kDoTemper) && threadIdx.x == 0) {
+      a.temperature_prev[t] = a.temperature[t];
+      tile_status(a, t, a.temperature[t]);
+    }
+    if (a.flags & kDoWeights) {
+      for (int i = threadIdx.x; i < N; i += NT) {
+        a.log_w[(size_t)t * N + i] = 0.0f;
+        a.weights[(size_t)t * N + i] = 1.0f / (float)N;
+      }
+      // a.ess[t] keeps the ESS of the tile's last step, as a single-tile
+      // run of the reference reports it after its final resample
+    }
+    if (a.flags & kDoResample)
+      for (int i = threadIdx.x; i < N; i += NT) a.idx[(size_t)t * N + i] = i;
+    return;
+  }
+  TileLL<NT, PER> ll;
+  if (a.flags & (kDoTemper | kDoWeights)) {
+    const float* llg = a.loglik + (size_t)t * N;
+#pragma unroll
+    for (int h = 0; h < VPT; ++h)
+#pragma unroll
+      for (int j = 0; j < PER; ++j)
+        ll.l[h][j] = ll.valid(h, j, N) ? llg[vthread<NT>(h) + j * kTB] : 0.f;
+  }
+
+  // ------------------------------------------------------------------ temper
+  float d_new = 0.f;  // float32 temperature increment, when tempered here
+  if (a.flags & kDoTemper) {
+    const float tau = a.temperature[t];
+    float lmv[VPT];
+#pragma unroll
+    for (int h = 0; h < VPT; ++h) {
+      lmv[h] = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < PER; ++j)
+        if (ll.valid(h, j, N)) lmv[h] = fmaxf(lmv[h], ll.l[h][j]);
+    }
+    const float lm = vblock_max<NT>(lmv, &red, parity);
+    SMC_TRACE(trow, 1);
+    const double thr = a.ess_threshold;
+    auto f = [&](double x) { return block_ess_objective(ll, N, lm, x, thr, &red, parity); };
+    const double top = 1.0 - (double)tau;
+    // sampler.py:113-122: root-find only if ESS at delta = 1 - tau is below threshold
+    const double ftop = f(top);
+    SMC_TRACE(trow, 2);
+    double delta = top;
+    // f(0) = N - thr exactly: every weight is exp(0) = 1
+    if (ftop < 0.0) delta = block_brentq(f, 0.0, top, (double)N - thr, ftop);
+    SMC_TRACE(trow, 3);
+    const float tnew = tau + (float)delta;  // delta tensor is float32 (sampler.py:105)
+    d_new = tnew - tau;
+    if (threadIdx.x == 0) {
+      a.temperature_prev[t] = tau;
+      a.temperature[t] = tnew;
+      tile_status(a, t, tnew);
+    }
+  }
+
+  // ------------------------------------------------------------ update weights
+  if (a.flags & kDoWeights) {
+    const float d = (a.flags & kDoTemper) ? d_new : a.temperature[t] - a.temperature_prev[t];
+    float* lwg = a.log_w + (size_t)t * N;
+    float* wg = a.weights + (size_t)t * N;
+    float e[VPT][PER];
+    float mxv[VPT];
+#pragma unroll
+    for (int h = 0; h < VPT; ++h) {
+      mxv[h] = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        e[h][j] = nan_to_num(d * ll.l[h][j], -INFINITY);
+        if (ll.valid(h, j, N)) {
+          lwg[vthread<NT>(h) + j * kTB] = e[h][j];
+          mxv[h] = fmaxf(mxv[h], e[h][j]);
+        }
+      }
+    }
+    const float mx = vblock_max<NT>(mxv, &red, parity);
+    double ssum[VPT];
+#pragma unroll
+    for (int h = 0; h < VPT; ++h) {
+      double s[PER];
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        e[h][j] = ll.valid(h, j, N) ? expf(e[h][j] - mx) : 0.f;
+        s[j] = (double)e[h][j];
+      }
+      ssum[h] = tree_sum(s);
+    }
+    const float sf = (float)vblock_sumd<NT>(ssum, &red, parity);
+    double qsum[VPT];
+#pragma unroll
+    for (int h = 0; h < VPT; ++h) {
+      double q[PER];
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const float wv = e[h][j] / sf;
+        q[j] = (double)wv * (double)wv;
+        if (ll.valid(h, j, N)) {
+          wg[vthread<NT>(h) + j * kTB] = wv;
+          buf[vthread<NT>(h) + j * kTB] = wv;
+        }
+      }
+      qsum[h] = tree_sum(q);
+    }
+    const double qs = vblock_sumd<NT>(qsum, &red, parity);
+    SMC_TRACE(trow, 4);
+    if (threadIdx.x == 0) {
+      a.ess[t] = (float)(1.0 / qs);
+      a.logZ[t] = (a.logZ[t] + mx) + logf(sf / (float)N);
+    }
+  }
+
+  // ---------------------------------------------------------- resample index
+  if (a.flags & kDoResample) {
+    if (!(a.flags & kDoWeights)) {
+      const float* W = a.weights + (size_t)t * N;
+      for (int i = threadIdx.x; i < N; i += NT) buf[i] = W[i];
+    }
+    __syncthreads();
+    // bins = cumsum(W): float64 running sum rounded per element to float32
+    // (what torch's CPU cumsum does), contiguous chunk per virtual thread, in place
+    const int chunk = (N + kTB - 1) / kTB;
+    // chunks of 8 (N = 4096) move as two 16-byte LDS accesses per thread
+    const bool vec8 = chunk == 8 && (N & 7) == 0;
+    int b0[VPT], b1[VPT];
+    float cv[VPT][8];
+    double part[VPT], incl[VPT];
+#pragma unroll
+    for (int h = 0; h < VPT; ++h) {
+      b0[h] = min(vthread<NT>(h) * chunk, N);
+      b1[h] = min(b0[h] + chunk, N);
+      part[h] = 0.0;
+      if (vec8) {
+        if (b0[h] < b1[h]) {
+          const float4 v0 = *reinterpret_cast<const float4*>(buf + b0[h]);
+          const float4 v1 = *reinterpret_cast<const float4*>(buf + b0[h] + 4);
+          cv[h][0] = v0.x; cv[h][1] = v0.y; cv[h][2] = v0.z; cv[h][3] = v0.w;
+          cv[h][4] = v1.x; cv[h][5] = v1.y; cv[h][6] = v1.z; cv[h][7] = v1.w;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) part[h] += (double)cv[h][i];
+        }
+      } else {
+        for (int i = b0[h]; i < b1[h]; ++i) part[h] += (double)buf[i];
+      }
+      incl[h] = part[h];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double y = __shfl_up(incl[h], o, kWave);
+        if (lane >= o) incl[h] += y;
+      }
+    }
+    const int k = parity;
+    parity ^= 1;
+#pragma unroll
+    for (int h = 0; h < VPT; ++h)
+      if (lane == 63) red.d[k][vwave<NT>(h)][0] = incl[h];
+    __syncthreads();
+    SMC_TRACE(trow, 5);
+#pragma unroll
+    for (int h = 0; h < VPT; ++h) {
+      double base = 0.0;
+      for (int i = 0; i < vwave<NT>(h); ++i) base += red.d[k][i][0];
+      double run = base + incl[h] - part[h];
+      if (vec8) {
+        if (b0[h] < b1[h]) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            run += (double)cv[h][i];
+            cv[h][i] = (float)run;
+          }
+          *reinterpret_cast<float4*>(buf + b0[h]) =
+              make_float4(cv[h][0], cv[h][1], cv[h][2], cv[h][3]);
+          *reinterpret_cast<float4*>(buf + b0[h] + 4) =
+              make_float4(cv[h][4], cv[h][5], cv[h][6], cv[h][7]);
+        }
+      } else {
+        for (int i = b0[h]; i < b1[h]; ++i) {
+          run += (double)buf[i];
+          buf[i] = (float)run;
+        }
+      }
+    }
+    __syncthreads();
+    float U = 0.f;
+    if (a.method == SMCDET_RESAMPLE_SYSTEMATIC) {
+      if (a.u) {
+        U = a.u[t];
+      } else {
+        const U4 r = philox4x32((uint32_t)a.offset, (uint32_t)(a.offset >> 32), (uint32_t)t,
+                                kTagResample, a.k0, a.k1);
+        U = u01(r.x);
+      }
+    }
+    const float total = buf[N - 1];
+    int64_t* idxg = a.idx + (size_t)t * N;
+    if (a.method == SMCDET_RESAMPLE_SYSTEMATIC) {
+      // bucketize(u, bins), u_n = (n + U) / N in float32 (sampler.py:144),
+      // right=False: idx[n] = #{i : bins[i] < u_n}.  With cnt(i) = #{n : u_n <= bins[i]}
+      // (monotone in i), idx[n] = #{i : cnt(i) <= n}: the last bin of every run of
+      // equal cnt writes i+1 to slot[cnt], and a prefix max over slots gives idx.
+      // Exact (u_n is recomputed with the same float ops) and load-balanced
+      // whatever the weight degeneracy, unlike a per-n search.
+      int* slot = reinterpret_cast<int*>(buf + N);  // N+1 ints
+      const float Nf = (float)N;
+      auto un = [&](int n) { return ((float)n + U) / Nf; };
+      // For N a power of two the division is an exact scaling:
+      // u_n <= b  <=>  fl(n + U) <= b*N (exact), and n <= fl(n + U) <= n + 1,
+      // so every n < floor(b*N) counts and only n = floor(b*N) needs a test.
+      const bool pow2 = (N & (N - 1)) == 0;
+      auto cnt = [&](float b) {
+        if (pow2) {
+          const float B = b * Nf;
+          int c = (int)fminf(fmaxf(floorf(B), 0.f), Nf);
+          c += (c < N && (float)c + U <= B) ? 1 : 0;
+          return c;
+        }
+        int c = (int)fminf(fmaxf(floorf(b * Nf - U), 0.f), Nf);
+        while (c > 0 && un(c - 1) > b) --c;
+        while (c < N && un(c) <= b) ++c;
+        return c;
+      };
+      for (int i = threadIdx.x; i <= N; i += NT) slot[i] = 0;
+      __syncthreads();
+      SMC_TRACE(trow, 6);
+      for (int i = threadIdx.x; i < N; i += NT) {
+        const int ci = cnt(buf[i]);
+        const int cnext = (i + 1 < N) ? cnt(buf[i + 1]) : -1;
+        if (cnext != ci) slot[ci] = i + 1;
+      }
+      __syncthreads();
+      SMC_TRACE(trow, 7);
+      // prefix max over slot[0..N-1], contiguous chunk per virtual thread
+      int sv[VPT][8];
+      int incl_m[VPT];
+#pragma unroll
+      for (int h = 0; h < VPT; ++h) {
+        int pm = 0;
+        if (vec8) {
+          if (b0[h] < b1[h]) {
+            const int4 v0 = *reinterpret_cast<const int4*>(slot + b0[h]);
+            const int4 v1 = *reinterpret_cast<const int4*>(slot + b0[h] + 4);
+            sv[h][0] = v0.x; sv[h][1] = v0.y; sv[h][2] = v0.z; sv[h][3] = v0.w;
+            sv[h][4] = v1.x; sv[h][5] = v1.y; sv[h][6] = v1.z; sv[h][7] = v1.w;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pm = max(pm, sv[h][i]);
+          }
+        } else {
+          for (int i = b0[h]; i < b1[h]; ++i) pm = max(pm, slot[i]);
+        }
+        incl_m[h] = pm;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(incl_m[h], o, kWave);
+          if (lane >= o) incl_m[h] = max(incl_m[h], y);
+        }
+      }
+      const int k2 = parity;
+      parity ^= 1;
+#pragma unroll
+      for (int h = 0; h < VPT; ++h)
+        if (lane == 63) red.i[k2][vwave<NT>(h)] = incl_m[h];
+      __syncthreads();
+#pragma unroll
+      for (int h = 0; h < VPT; ++h) {
+        int run_m = __shfl_up(incl_m[h], 1, kWave);
+        if (lane == 0) run_m = 0;
+        for (int i = 0; i < vwave<NT>(h); ++i) run_m = max(run_m, red.i[k2][i]);
+        // in place: slot[i] becomes idx[i] (each virtual thread owns its chunk)
+        if (vec8) {
+          if (b0[h] < b1[h]) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              run_m = max(run_m, sv[h][i]);
+              sv[h][i] = min(run_m, N - 1);
+            }
+            *reinterpret_cast<int4*>(slot + b0[h]) =
+                make_int4(sv[h][0], sv[h][1], sv[h][2], sv[h][3]);
+            *reinterpret_cast<int4*>(slot + b0[h] + 4) =
+                make_int4(sv[h][4], sv[h][5], sv[h][6], sv[h][7]);
+          }
+        } else {
+          for (int i = b0[h]; i < b1[h]; ++i) {
+            run_m = max(run_m, slot[i]);
+            slot[i] = min(run_m, N - 1);
+          }
+        }
+      }
+      __syncthreads();
+      SMC_TRACE(trow, 8);
+      for (int n = threadIdx.x; n < N; n += NT) idxg[n] = (int64_t)slot[n];
+      SMC_TRACE(trow, 9);
+    } else {
+      // multinomial (sampler.py:127-140): target = u * total, first bin > target
+      for (int n = threadIdx.x; n < N; n += NT) {
+        float un;
+        if (a.u) {
+          un = a.u[(size_t)t * N + n];
+        } else {
+          const uint64_t c = a.offset + (uint64_t)n;
+          const U4 r = philox4x32((uint32_t)c, (uint32_t)(c >> 32), (uint32_t)t,
+                                  kTagResample + 1, a.k0, a.k1);
+          un = u01(r.x);
+        }
+        const float target = un * total;
+        int lo = 0, hi = N;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (buf[mid] > target) hi = mid; else lo = mid + 1;
+        }
+        idxg[n] = (int64_t)min(lo, N - 1);
+      }
+    }
+  }
+}
+
+// LDS words tile_work needs in `buf`
+__host__ __device__ inline size_t tile_lds_bytes(int N) { return (size_t)(2 * N + 1) * sizeof(float); }
+
+}  // namespace smcdet

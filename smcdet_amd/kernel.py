@@ -96,7 +96,7 @@ class SingleComponentMH(object):
 
     def run(self, data, counts, locs, fluxes, temperature, log_target=None, *, prior=None,
             image_model=None, ancestors=None, replay=None, want_loglik=True, rate_in=None,
-            rate_out=None, flags=0, go=None, tile_boxes=None):
+            rate_out=None, flags=0, go=None, tile_boxes=None, tail=None, tail_take=0):
         """kernel.py:26-130.  ancestors [numH,numW,N] (int64, optional) gathers
         the starting state (a fused resample); replay = dict(comp, uloc, uflux,
         uacc) replays recorded draws; rate_in / rate_out [numH,numW,N,H*W]
@@ -105,15 +105,26 @@ class SingleComponentMH(object):
         (ignored in full_recompute mode).  go (int32 device scalar, optional):
         the launch does nothing when *go == 0 (speculative enqueue, see
         SMCsampler.run).  tile_boxes [T,4] (optional): each tile's own
-        location box (Prior pad_mode "partition")."""
+        location box (Prior pad_mode "partition").  tail (smcdet_smc_tail_t,
+        optional; SingleComponentMH only): the temper / reweight / next
+        resampling pass that follows in SMCsampler.run, run by the same
+        launch (smcdet_mh_sweep_step) on the returned log-likelihoods;
+        `temperature` is then updated in place; tail_take counters of the
+        random stream are reserved for its resampling right after the
+        sweep's own (tail.offset), the order of the separate launches."""
         prior, image_model = self._resolve(log_target, prior, image_model)
         data = _hip.dev_f32(data, "data")
         counts = _hip.dev_f32(counts, "counts")
         locs = _hip.dev_f32(locs, "locs")
         fluxes = _hip.dev_f32(fluxes, "fluxes")
         dev = locs.device
+        temperature_arg = temperature
         temperature = _hip.dev_f32(torch.as_tensor(temperature, device=dev, dtype=torch.float32),
                                    "temperature")
+        if tail is not None and not (isinstance(temperature_arg, torch.Tensor) and
+                                     temperature.data_ptr() == temperature_arg.data_ptr()):
+            raise ValueError("the fused SMC step updates `temperature` in place: pass the "
+                             "sampler's contiguous float32 device tensor")
         nH, nW, N, S, _ = locs.shape
         T = nH * nW
         if temperature.numel() != T:
@@ -140,6 +151,8 @@ class SingleComponentMH(object):
             rp = _hip.ReplayC(_hip.ptr(rc).value, _hip.ptr(ru[0]).value, _hip.ptr(ru[1]).value,
                               _hip.ptr(ru[2]).value)
         off = self.rng.take(self.num_iters)
+        if tail is not None and tail_take:
+            tail.offset = self.rng.take(tail_take)
         cm, cp, ch = image_model._cmodel(), prior._cprior(), self._cmh(prior)
         extra_flags = flags
         flags = (_hip.SMCDET_MH_FULL_RECOMPUTE if self.full_recompute else 0) | self.debug_flags
@@ -154,11 +167,20 @@ class SingleComponentMH(object):
         elif tile_boxes is not None:
             raise NotImplementedError(f"{type(self).__name__}: per-tile location boxes "
                                       "(pad_mode='partition') need SingleComponentMH")
+        entry = self._entry
+        if tail is not None:
+            if entry != "smcdet_mh_sweep":
+                raise NotImplementedError(f"{type(self).__name__}: the fused SMC step runs "
+                                          "SingleComponentMH sweeps")
+            if ll is None:
+                raise ValueError("the fused SMC step needs want_loglik=True")
+            entry = "smcdet_mh_sweep_step"
+            extra = extra + [_hip.ref(tail)]
         ev = self.launch_events
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(torch.cuda.current_stream(dev))
-        _hip.check(getattr(_hip.lib(), self._entry)(
+        _hip.check(getattr(_hip.lib(), entry)(
             _hip.ref(cm), _hip.ref(cp), _hip.ref(ch), _hip.ptr(data), _hip.ptr(temperature),
             T, N, S, anc_p, _hip.ptr(counts), _hip.ptr(locs), _hip.ptr(fluxes),
             _hip.ptr(counts_out), _hip.ptr(locs_out), _hip.ptr(fluxes_out),
@@ -166,7 +188,7 @@ class SingleComponentMH(object):
             _hip.ptr(self._rate_buffer(rate_out, "rate_out", T * N, data)),
             self.rng.seed, off,
             _hip.ref(rp) if rp is not None else None, flags, _hip.ptr(ll), _hip.ptr(acc),
-            _hip.ptr(acc_ws), _hip.ptr(go), *extra, _hip.stream_of(locs)), self._entry)
+            _hip.ptr(acc_ws), _hip.ptr(go), *extra, _hip.stream_of(locs)), entry)
         if ev is not None:
             e1.record(torch.cuda.current_stream(dev))
             ev.append((e0, e1))

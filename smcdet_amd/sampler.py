@@ -269,8 +269,9 @@ class SMCsampler(object):
         rin = None if fresh else self._rate[self._rate_cur]
         return rin, self._rate[1 - self._rate_cur]
 
-    def mutate(self, ancestors=None):
-        """sampler.py:171-179."""
+    def mutate(self, ancestors=None, **fused):
+        """sampler.py:171-179.  (fused: tail / tail_take of the fused SMC
+        step, _step.)"""
         rin, rout = self._rate_buffers()
         kw = {} if rout is None else {"rate_in": rin, "rate_out": rout}
         if self.stopping == "independent":
@@ -279,6 +280,7 @@ class SMCsampler(object):
             kw["go"] = self._go
         if self.tile_boxes is not None:
             kw["tile_boxes"] = self.tile_boxes
+        kw.update(fused)
         self.locs, self.fluxes, self.mutation_acc_rates = self.MutationKernel.run(
             self.tiled_image, self.counts, self.locs, self.fluxes, self.temperature,
             self.log_target, ancestors=ancestors, **kw)
@@ -293,18 +295,19 @@ class SMCsampler(object):
             self.counts = self.MutationKernel.last_counts
         self._fresh_loglik = self.MutationKernel.last_loglik
 
-    def _temper_reweight(self, with_resample):
-        """temper + update_weights (+ next resampling indices), one launch."""
-        self.loglik = self._current_loglik()
-        N = self.loglik.shape[-1]
-        # temperature / log Z are updated in place by the kernel (no per-step
-        # device copies); temperature_prev is a second persistent buffer
+    def _tr_prepare(self, with_resample):
+        """Output buffers of the temper / reweight (/ next resampling indices)
+        pass, shared by its own launch (_temper_reweight) and the fused step
+        (_step).  temperature / log Z are updated in place by the kernel (no
+        per-step device copies); temperature_prev is a second persistent
+        buffer."""
         new_t = self.temperature
+        shape = tuple(self.counts.shape)
         prev_t = getattr(self, "temperature_prev", None)
         if prev_t is None or prev_t is new_t or prev_t.shape != new_t.shape:
             prev_t = torch.empty_like(new_t)
-        self.weights_log_unnorm = torch.empty_like(self.loglik)
-        self.weights = torch.empty_like(self.loglik)
+        self.weights_log_unnorm = torch.empty(shape, device=new_t.device, dtype=torch.float32)
+        self.weights = torch.empty_like(self.weights_log_unnorm)
         if self.stopping != "independent" or getattr(self, "ess", None) is None or \
                 self.ess.shape != new_t.shape:
             self.ess = torch.empty_like(new_t)
@@ -312,10 +315,23 @@ class SMCsampler(object):
         # ESS of its last step)
         live = self._live_ws()
         idx = None
-        off = 0
         if with_resample:
-            idx = torch.empty(self.loglik.shape, device=self.device, dtype=torch.int64)
-            off = self._resample_offset(N)
+            idx = torch.empty(shape, device=new_t.device, dtype=torch.int64)
+        return prev_t, live, idx
+
+    def _tr_finish(self, prev_t, live, idx):
+        self.temperature_prev = prev_t
+        self._pending_idx = idx
+        self._live = live
+        self._live_valid = True
+
+    def _temper_reweight(self, with_resample):
+        """temper + update_weights (+ next resampling indices), one launch."""
+        self.loglik = self._current_loglik()
+        N = self.loglik.shape[-1]
+        prev_t, live, idx = self._tr_prepare(with_resample)
+        off = self._resample_offset(N) if with_resample else 0
+        new_t = self.temperature
         _hip.check(_hip.lib().smcdet_temper_reweight(
             _hip.ptr(self.loglik), _hip.ptr(new_t), _hip.ptr(prev_t),
             _hip.ptr(self.weights_log_unnorm), _hip.ptr(self.weights), _hip.ptr(self.ess),
@@ -325,11 +341,59 @@ class SMCsampler(object):
             _hip.ptr(self.iters_per_tile), int(getattr(self, "iter", 0)), _hip.ptr(live),
             _hip.ptr(getattr(self, "_go", None)), getattr(self, "_live_host", None),
             _hip.stream_of(new_t)), "smcdet_temper_reweight")
-        self.temperature_prev = prev_t
-        self.temperature = new_t
-        self._pending_idx = idx
-        self._live = live
-        self._live_valid = True
+        self._tr_finish(prev_t, live, idx)
+
+    # True: SMC iterations run as one launch (smcdet_mh_sweep_step: the MH
+    # sweep's last workgroup per tile tempers, reweights and draws the next
+    # indices); False: the sweep and the tile pass as two launches (A/B).
+    # Same results either way.
+    fused_step = True
+
+    def _step_fusable(self):
+        return (self.fused_step and self.fused
+                and getattr(self.MutationKernel, "_entry", None) == "smcdet_mh_sweep"
+                and all(h not in self.__dict__ and getattr(type(self), h) is getattr(SMCsampler, h)
+                        for h in ("mutate", "_temper_reweight", "_current_loglik")))
+
+    def _step(self, idx, resample_u=None, replay=None):
+        """One SMC iteration of the fused schedule (sampler.py:221-237: the
+        resampling gather of idx, mutate, temper, update_weights, the next
+        resampling indices).  Tests: resample_u [numH,numW] replays the next
+        systematic offsets, replay the MH draws (SingleComponentMH.run)."""
+        if not self._step_fusable():
+            if resample_u is not None or replay is not None:
+                raise ValueError("resample_u / replay need the fused step")
+            self.mutate(ancestors=idx)
+            self._temper_reweight(with_resample=True)
+            return
+        N = self.counts.shape[-1]
+        prev_t, live, idx_next = self._tr_prepare(True)
+        tail = _hip.SmcTailC()
+        tail.temperature_prev = _hip.ptr(prev_t)
+        tail.log_weights_unnorm = _hip.ptr(self.weights_log_unnorm)
+        tail.weights = _hip.ptr(self.weights)
+        tail.ess = _hip.ptr(self.ess)
+        tail.log_norm_const = _hip.ptr(self.log_normalizing_constant)
+        tail.ess_threshold = float(self.ess_threshold)
+        tail.resample_method = self._method_code()
+        tail.flags = _hip.SMCDET_SMC_FREEZE_DONE if self.stopping == "independent" else 0
+        tail.seed = self.rng.seed
+        tail.idx = _hip.ptr(idx_next)
+        ru = None
+        if resample_u is not None:
+            ru = _hip.dev_f32(torch.as_tensor(resample_u, device=self.device,
+                                              dtype=torch.float32), "resample_u")
+            tail.resample_u = _hip.ptr(ru)
+        tail.finished_iter = _hip.ptr(getattr(self, "iters_per_tile", None))
+        tail.live = _hip.ptr(live)
+        tail.live_host = getattr(self, "_live_host", None)
+        tail.iter = int(getattr(self, "iter", 0))
+        take = 1 if self.resample_method == "systematic" else N
+        extra = {} if replay is None else {"replay": replay}
+        self.mutate(ancestors=idx, tail=tail, tail_take=take, **extra)
+        del ru
+        self.loglik = self._fresh_loglik
+        self._tr_finish(prev_t, live, idx_next)
 
     def _live_ws(self):
         """The next of two [3] int32 buffers (zeroed once, alternating per
@@ -462,8 +526,7 @@ class SMCsampler(object):
                 self._go = live_prev[2:3]
                 self._live_host = pinned.dev(1 - slot)
                 idx, self._pending_idx = self._pending_idx, None
-                self.mutate(ancestors=idx)
-                self._temper_reweight(with_resample=True)
+                self._step(idx)
                 self._go = self._live_host = None
                 ev = launched()
                 if ev_prev is not None:
@@ -520,8 +583,7 @@ class SMCsampler(object):
                 self.iter += 1
                 self._print_progress()
                 idx, self._pending_idx = self._pending_idx, None
-                self.mutate(ancestors=idx)
-                self._temper_reweight(with_resample=True)
+                self._step(idx)
                 if self.on_iteration is not None:
                     self.on_iteration(self)
         else:

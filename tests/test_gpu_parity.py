@@ -235,7 +235,9 @@ def test_prune_bit_exact():
 
 def _replay_smc(d, fused_mh_gather):
     """Drives smcdet_amd.SMCsampler method by method with the reference's
-    recorded draws (prior uniforms, systematic offsets, MH draws)."""
+    recorded draws (prior uniforms, systematic offsets, MH draws).
+    fused_mh_gather "step": SMCsampler._step (smcdet_mh_sweep_step), the next
+    iteration's systematic offset replayed into the step's resampling."""
     from smcdet_amd.sampler import SMCsampler
     draws = O.DrawStream(d)
     S, K, Np, td = int(d["S"]), int(d["K"]), int(d["N"]), int(d["tile_dim"])
@@ -254,10 +256,14 @@ def _replay_smc(d, fused_mh_gather):
     s.update_weights()
     s.iter = 0
     trace = [N(s.temperature)]
+    step = fused_mh_gather == "step"
+    if step:
+        idx = s.resample_index(u=T(draws.next("rand")))
     while bool((s.temperature < 1).any()) and s.iter <= s.max_smc_iters:
         s.iter += 1
-        U = draws.next("rand")
-        idx = s.resample_index(u=T(U))
+        if not step:
+            U = draws.next("rand")
+            idx = s.resample_index(u=T(U))
         comp, ul, uf, ua = [], [], [], []
         for _ in range(K):
             m = draws.next("mask")
@@ -269,6 +275,11 @@ def _replay_smc(d, fused_mh_gather):
             ua.append(ra)
         replay = dict(comp=torch.as_tensor(np.stack(comp)), uloc=torch.as_tensor(np.stack(ul)),
                       uflux=torch.as_tensor(np.stack(uf)), uacc=torch.as_tensor(np.stack(ua)))
+        if step:
+            s._step(idx, resample_u=T(draws.next("rand")), replay=replay)
+            idx = s._pending_idx
+            trace.append(N(s.temperature))
+            continue
         if fused_mh_gather:
             anc = idx
         else:
@@ -283,13 +294,16 @@ def _replay_smc(d, fused_mh_gather):
         s.temper()
         s.update_weights()
         trace.append(N(s.temperature))
-    U = draws.next("rand")
-    s._gather(s.resample_index(u=T(U)))
+    if step:
+        s._gather(idx)
+    else:
+        U = draws.next("rand")
+        s._gather(s.resample_index(u=T(U)))
     pc, pl, pf = s.prune(s.locs, s.fluxes)
     return s, np.stack(trace), pc
 
 
-@pytest.mark.parametrize("fused", [False, True], ids=["gather", "mh-gather"])
+@pytest.mark.parametrize("fused", [False, True, "step"], ids=["gather", "mh-gather", "mh-step"])
 @pytest.mark.parametrize("name", ["smc_replay_m71_8x8", "smc_replay_m71_tiles"])
 def test_smc_end_to_end_replay_vs_reference(name, fused):
     """Whole SMC run driven by the reference's recorded draws.  Both fixtures'
