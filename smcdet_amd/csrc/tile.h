@@ -232,6 +232,7 @@ template <int NT, int PER>
 __device__ __forceinline__ double block_ess_objective(const TileLL<NT, PER>& ll, int N, float lmax,
                                                       double delta, double thr, TileRed* red,
                                                       int& parity) {
+#pragma clang fp contract(off)
   constexpr int VPT = VLayout<NT>::VPT;
   const float df = (float)delta;
   const float m = df * lmax;  // = max_i fl(df*l_i): rounding is monotone
@@ -260,6 +261,7 @@ __device__ __forceinline__ double block_ess_objective(const TileLL<NT, PER>& ll,
 // values; the workgroup evaluates f together.
 template <class F>
 __device__ double block_brentq(F&& f, double xa, double xb, double fa, double fb) {
+#pragma clang fp contract(off)
   const double xtol = 1e-6, rtol = 1e-6;
   double xpre = xa, xcur = xb, xblk = 0., fpre = fa, fcur = fb, fblk = 0., spre = 0., scur = 0.;
   if (fpre == 0.0) return xpre;
@@ -312,6 +314,7 @@ __device__ double block_brentq(F&& f, double xa, double xb, double fa, double fb
 template <int NT, int PER>
 __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, TileRed& red,
                                           [[maybe_unused]] int trow) {
+#pragma clang fp contract(off)
   constexpr int VPT = VLayout<NT>::VPT;
   int parity = 0;
   const int N = a.N;
