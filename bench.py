@@ -93,9 +93,12 @@ def parse():
     ap.add_argument("--no-full-run", action="store_true")
     # skip the untimed comparison with the reference's recorded runs
     ap.add_argument("--no-vs-ref", action="store_true")
-    # A/B: the sweep and the temper/reweight/resample pass as two launches
-    # instead of one fused launch (SMCsampler.fused_step)
-    ap.add_argument("--split-step", action="store_true")
+    # A/B: the temper/reweight/resample pass inside the sweep's launch
+    # (SMCsampler.fused_step) instead of the default two back-to-back launches
+    ap.add_argument("--fused-step", action="store_true")
+    # no kernel-timing pass after the timed region (the roofline then uses the
+    # step time as the kernel time)
+    ap.add_argument("--no-kernel-timing", action="store_true")
     return ap.parse_args()
 
 
@@ -576,13 +579,13 @@ def main():
             tdist.destroy_process_group()
         return
     s, mh, steps_per_step, cpu_tile, cfg = build_sampler(args, dev, rank)
-    s.fused_step = not args.split_step
+    s.fused_step = args.fused_step
     s.initialize()
-    cfg = dict(cfg, step="split" if args.split_step else (
-        "fused" if s._step_fusable() and _hip_fused(s) else "split (shape)"))
+    cfg = dict(cfg, step="two launches" if not args.fused_step else (
+        "fused" if s._step_fusable() and _hip_fused(s) else "two launches (shape)"))
     s._temper_reweight(with_resample=True)
 
-    ev = []
+    from smcdet_amd import _hip
 
     def step():
         # one SMC iteration: the MH sweep from the ancestors, then temper /
@@ -592,9 +595,6 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    # HIP events recorded on the launch stream right around each MH sweep
-    # launch (smcdet_mh_sweep = one kernel): the roofline's kernel duration
-    mh.launch_events = ev
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
@@ -603,16 +603,31 @@ def main():
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    mh.launch_events = None
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
+    # The roofline's kernel duration: the next `steps` SMC steps again, each
+    # sweep launch timed by HIP events stamped on its own dispatch packet
+    # (hipExtLaunchKernel, smcdet_launch_timing).  Not inside the timed
+    # region: any per-launch timing (these events or hipEventRecord markers)
+    # leaves a 7-10 us bubble before the next launch (rocprofv3 kernel traces,
+    # profiles/r02_s3_gap_bench.txt), while untimed back-to-back launches run
+    # gap-free.
+    if args.no_kernel_timing:
+        ev = [elapsed * 1e3 / args.steps]
+    else:
+        _hip.launch_timing(args.steps)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        ev = _hip.launch_timing_read(args.steps)
+        _hip.launch_timing(0)
     if dist:
         t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu",
                          dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t)
-    mh_ms = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
+    mh_ms = sum(ev) / max(len(ev), 1)
 
     if args.total_tiles > 0:  # strong scaling: every rank's tiles, uneven shares included
         value = args.total_tiles * args.particles * args.mh_iters * args.steps / elapsed
@@ -658,6 +673,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": f"smcdet {args.kernel}_sweep_kernel", "kernel_ms": mh_ms,
+                     "kernel_timing": ("step time (no timing pass)" if args.no_kernel_timing
+                                       else f"HIP dispatch events, {len(ev)} launches right "
+                                            "after the timed region"),
                      "alg_bytes_per_particle_step": b_alg},
         "compute": compute_block(args, mh_rate, f_alg, launch_steps, mh_ms),
         "smc": {"temperature_min": float(s.temperature.min()),

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 13
+#define SMCDET_ABI_VERSION 14
 
 /* status codes */
 #define SMCDET_OK 0
@@ -73,6 +73,13 @@ extern "C" {
  * Without it (the reference, sampler.py:230) such tiles are resampled and
  * mutated at temperature 1 until every tile has finished. */
 #define SMCDET_SMC_FREEZE_DONE 1u
+/* smcdet_mh_sweep_step only: run the tile pass as its own launch right after
+ * the sweep even where the shape could fuse (same results).  The default in
+ * SMCsampler: on gfx950 the separate 512-thread tile kernel (~27 us at
+ * N = 4096) beats the fused tail on the sweep's 256-thread workgroup (~30 us),
+ * and back-to-back launches on one stream leave no gap to recover
+ * (DESIGN.md §4.2). */
+#define SMCDET_SMC_TWO_LAUNCH 2u
 /* diagnostic ablations (timing only; results are NOT valid samples) */
 #define SMCDET_MH_ABLATE_LIKELIHOOD 256u /* skip the delta-likelihood passes */
 #define SMCDET_MH_ABLATE_PROPOSAL 512u   /* skip the truncated-normal proposal math */
@@ -137,6 +144,18 @@ const char* smcdet_last_error(void);
  * live_host).  Free with smcdet_host_free(host). */
 int smcdet_host_alloc(size_t bytes, void** host, void** device);
 int smcdet_host_free(void* host);
+
+/* Per-launch kernel timing for benchmarks (no reference counterpart).  While
+ * enabled, each of the next max_launches sweep launches (smcdet_mh_sweep,
+ * smcdet_mh_sweep_step, smcdet_mala_sweep) is dispatched by
+ * hipExtLaunchKernel with a start/stop event pair of an internal pool: the
+ * events are stamped by the kernel's own dispatch, so timing adds no marker
+ * packet (and no launch bubble) between kernels.  max_launches = 0 disables
+ * timing and frees the pool; a new call discards earlier timings.
+ * smcdet_launch_timing_read waits for the timed launches and writes the first
+ * min(max, *n_out) durations in ms; *n_out = launches timed since enabling. */
+int smcdet_launch_timing(int32_t max_launches);
+int smcdet_launch_timing_read(float* ms, int32_t max, int32_t* n_out);
 
 /* ImageModel.loglikelihood / M71ImageModel.loglikelihood
  * (smcdet/images.py:85-102, :159-175): out[T,N]. */

@@ -51,9 +51,26 @@ def main():
         s._temper_reweight(with_resample=True)
     torch.cuda.synchronize()
     wall = (time.perf_counter() - a) / n
+    # the fused step (SMCsampler._step: one launch)
+    t_step = []
+    for i in range(40):
+        idx, s._pending_idx = s._pending_idx, None
+        a = time.perf_counter()
+        s._step(idx)
+        if i >= 5:
+            t_step.append(time.perf_counter() - a)
+    torch.cuda.synchronize()
+    a = time.perf_counter()
+    for _ in range(n):
+        idx, s._pending_idx = s._pending_idx, None
+        s._step(idx)
+    torch.cuda.synchronize()
+    wall_fused = (time.perf_counter() - a) / n
     out = {"host_mutate_us": 1e6 * sum(t_mut) / len(t_mut),
            "host_temper_reweight_us": 1e6 * sum(t_tr) / len(t_tr),
-           "wall_per_step_us": 1e6 * wall}
+           "wall_per_step_us": 1e6 * wall,
+           "host_fused_step_us": 1e6 * sum(t_step) / len(t_step),
+           "wall_per_fused_step_us": 1e6 * wall_fused}
     print(json.dumps(out))
 
 

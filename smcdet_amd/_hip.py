@@ -23,8 +23,9 @@ SMCDET_RESAMPLE_SYSTEMATIC = 1
 SMCDET_MH_FULL_RECOMPUTE = 1
 SMCDET_MH_COMPONENT_BY_COUNT = 2
 SMCDET_MH_SKIP_DONE = 4
-ABI_VERSION = 13
+ABI_VERSION = 14
 SMCDET_SMC_FREEZE_DONE = 1
+SMCDET_SMC_TWO_LAUNCH = 2
 
 # Shapes the kernels support (checked by the C ABI too; the samplers raise
 # ValueError at construction with these named, SMCsampler/MHsampler.__init__):
@@ -100,6 +101,8 @@ _SIGS = {
     "smcdet_abi_version": ([], c_i),
     "smcdet_host_alloc": ([ctypes.c_size_t, c_p, c_p], c_i),
     "smcdet_host_free": ([c_p], c_i),
+    "smcdet_launch_timing": ([c_i], c_i),
+    "smcdet_launch_timing_read": ([c_p, c_i, c_p], c_i),
     "smcdet_last_error": ([], ctypes.c_char_p),
     "smcdet_loglik": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
     "smcdet_render": ([c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
@@ -180,11 +183,14 @@ def lib():
                 f"smcdet_amd: HIP library not found at {LIB_PATH}; build it with `make` "
                 "(or __graft_entry__.build())")
         L = ctypes.CDLL(LIB_PATH)
+        stale_ok = os.environ.get("SMCDET_ALLOW_STALE") == "1"
         for name, (args, res) in _SIGS.items():
+            if stale_ok and not hasattr(L, name):
+                continue  # an older library in a same-box A/B (entry point absent)
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
-        if os.environ.get("SMCDET_ALLOW_STALE") != "1":
+        if not stale_ok:
             src, built = source_hash(), built_hash(L)
             if src is not None and built != src:
                 raise RuntimeError(
@@ -202,6 +208,21 @@ def check(rc: int, what: str):
     if rc != 0:
         msg = lib().smcdet_last_error().decode()
         raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def launch_timing(max_launches: int):
+    """Time the next max_launches sweep launches on their own dispatch packets
+    (smcdet_launch_timing; 0 disables)."""
+    check(lib().smcdet_launch_timing(int(max_launches)), "smcdet_launch_timing")
+
+
+def launch_timing_read(max_launches: int):
+    """Durations (ms) of the sweep launches timed since launch_timing()."""
+    buf = (ctypes.c_float * max(int(max_launches), 1))()
+    n = c_i(0)
+    check(lib().smcdet_launch_timing_read(ctypes.addressof(buf), int(max_launches),
+                                          ctypes.byref(n)), "smcdet_launch_timing_read")
+    return [float(buf[i]) for i in range(min(n.value, int(max_launches)))]
 
 
 def ptr(t):

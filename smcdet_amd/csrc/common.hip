@@ -35,6 +35,25 @@ int ensure_lds(const void* kernel, size_t bytes) {
   return SMCDET_OK;
 }
 
+// ---- launch timing pool (smcdet_launch_timing / _read) ----------------------
+static hipEvent_t* g_tev = nullptr;  // 2 * g_tcap events: (start, stop) per launch
+static int g_tcap = 0, g_tused = 0;
+
+bool timing_next(hipEvent_t* start, hipEvent_t* stop) {
+  if (g_tused >= g_tcap) return false;
+  *start = g_tev[2 * g_tused];
+  *stop = g_tev[2 * g_tused + 1];
+  ++g_tused;
+  return true;
+}
+
+static void timing_free() {
+  for (int i = 0; i < 2 * g_tcap; ++i) (void)hipEventDestroy(g_tev[i]);
+  delete[] g_tev;
+  g_tev = nullptr;
+  g_tcap = g_tused = 0;
+}
+
 int validate_model(const smcdet_image_model_t* m) {
   if (!m) return set_error(SMCDET_EINVAL, "image model is null");
   if (m->model != SMCDET_MODEL_M71 && m->model != SMCDET_MODEL_POISSON)
@@ -120,6 +139,35 @@ int validate_prior(const smcdet_prior_t* p) {
 }  // namespace smcdet
 
 extern "C" {
+
+int smcdet_launch_timing(int32_t max_launches) {
+  smcdet::timing_free();
+  if (max_launches < 0) return smcdet::set_error(SMCDET_EINVAL, "max_launches < 0");
+  if (max_launches == 0) return SMCDET_OK;
+  smcdet::g_tev = new hipEvent_t[2 * (size_t)max_launches];
+  for (int i = 0; i < 2 * max_launches; ++i) {
+    if (hipEventCreate(&smcdet::g_tev[i]) != hipSuccess) {
+      for (int k = 0; k < i; ++k) (void)hipEventDestroy(smcdet::g_tev[k]);
+      delete[] smcdet::g_tev;
+      smcdet::g_tev = nullptr;
+      return smcdet::set_error(SMCDET_EHIP, "hipEventCreate failed");
+    }
+  }
+  smcdet::g_tcap = max_launches;
+  smcdet::g_tused = 0;
+  return SMCDET_OK;
+}
+
+int smcdet_launch_timing_read(float* ms, int32_t max, int32_t* n_out) {
+  const int n = smcdet::g_tused < max ? smcdet::g_tused : max;
+  for (int i = 0; i < n; ++i) {
+    if (hipEventSynchronize(smcdet::g_tev[2 * i + 1]) != hipSuccess ||
+        hipEventElapsedTime(&ms[i], smcdet::g_tev[2 * i], smcdet::g_tev[2 * i + 1]) != hipSuccess)
+      return smcdet::set_error(SMCDET_EHIP, "launch %d: event timing failed", i);
+  }
+  if (n_out) *n_out = smcdet::g_tused;
+  return SMCDET_OK;
+}
 
 #ifndef SMCDET_SRC_HASH
 #define SMCDET_SRC_HASH "unknown"

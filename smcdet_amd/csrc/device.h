@@ -5,6 +5,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include "../../include/smcdet_hip.h"
@@ -86,6 +87,19 @@ int set_error(int code, const char* fmt, ...);
 int check_launch(const char* what);
 // raises the kernel's dynamic-LDS limit when bytes > 64 KiB (<= 160 KiB)
 int ensure_lds(const void* kernel, size_t bytes);
+// launch timing (smcdet_launch_timing): the next start / stop event pair of
+// the pool, or false (nulls) when timing is off or the pool is used up
+bool timing_next(hipEvent_t* start, hipEvent_t* stop);
+// A sweep launch whose timing events (if any) ride on its own dispatch packet
+// (hipExtLaunchKernel): no marker packet between kernels, so timing does not
+// open a launch bubble in the step it measures.
+template <typename... Args, typename F = void (*)(Args...)>
+inline void launch_sweep(F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st,
+                         Args... args) {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  timing_next(&e0, &e1);
+  hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, st, e0, e1, 0u, args...);
+}
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al. 2011) — counter (c0..c3), key (k0,k1)

@@ -374,9 +374,9 @@ static int launch_mala(const MalaArgs& a, bool replay, dim3 grid, size_t lds, hi
   int rc = ensure_lds(fn, lds);
   if (rc) return rc;
   if (replay)
-    hipLaunchKernelGGL((mala_sweep_kernel<MODEL, true>), grid, dim3(kMalaBlock), lds, st, a);
+    launch_sweep(mala_sweep_kernel<MODEL, true>, grid, dim3(kMalaBlock), lds, st, a);
   else
-    hipLaunchKernelGGL((mala_sweep_kernel<MODEL, false>), grid, dim3(kMalaBlock), lds, st, a);
+    launch_sweep(mala_sweep_kernel<MODEL, false>, grid, dim3(kMalaBlock), lds, st, a);
   return SMCDET_OK;
 }
 

@@ -224,7 +224,10 @@ constexpr int mh_waves_per_eu() { return PPL == 1 ? SMCDET_SMALL_TILE_WAVES : 4;
 template <int PPL>
 constexpr int mh_slots() { return PPL == 1 ? 1 : kSlots; }
 
-template <int MODEL, bool REPLAY, bool FULL, int PPL, bool PAIRED>
+// TAIL: the fused SMC step's instantiation (a.has_tail); the sweep alone
+// compiles without the tail pass, which would otherwise raise its SGPR
+// pressure (spills reloaded by v_readlane in the loop).
+template <int MODEL, bool REPLAY, bool FULL, int PPL, bool PAIRED, bool TAIL>
 __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_kernel(MhArgs a) {
   constexpr int NSL = mh_slots<PPL>();
   extern __shared__ float smem[];
@@ -754,15 +757,24 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   // in (the ticket above); its LDS (rate images written back) becomes the
   // tile pass's buffer.  Not for 8x8 tiles: their 7 workgroups per CU cannot
   // hold the 2N+1-word buffer (the host launches the tile kernel instead).
-  if constexpr (PPL != 1 && !FULL && PAIRED) {
-    if (a.has_tail) {
+  if constexpr (TAIL && PPL != 1 && !FULL && PAIRED) {
+    {
       __shared__ TileRed tail_red;
       __syncthreads();
       if (wg_last) {
         // acquire: the other workgroups' loglik_out stores (released by their
         // device-scope fence before the ticket)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        tile_work<kMhBlock, 8>(a.tail, t, smem, tail_red, -1);
+        // the tail's arguments are read only here: the opaque pointer keeps
+        // the compiler from hoisting their kernarg loads above the sweep,
+        // where they would stay live in SGPRs across the MH loop (spills)
+        // (MhArgs is the kernel's only argument: offset 0 of the kernarg
+        // segment; taking &a.tail instead would copy all of `a` to scratch)
+        const TileArgs* tp = reinterpret_cast<const TileArgs*>(
+            (const char*)__builtin_amdgcn_kernarg_segment_ptr() +
+            offsetof(MhArgs, tail));
+        __asm__ volatile("" : "+s"(tp));
+        tile_work<kMhBlock, 8>(*tp, t, smem, tail_red, -1);
       }
     }
   }
@@ -773,16 +785,21 @@ static int launch_mh1(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
   // FULL mode never evaluates union-window slots: one instantiation
   constexpr bool kPair = !FULL;
   const bool paired = kPair && !a.scalar_slots;
-  const void* fn = paired ? (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair>
-                          : (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, false>;
+  // the fused tail exists only where tail_fusable() allows it
+  constexpr bool kTail = !FULL && PPL != 1;
+  const bool tail = kTail && paired && a.has_tail;
+  if (a.has_tail && !tail) return set_error(SMCDET_EINVAL, "fused step: unsupported shape");
+  const void* fn = tail     ? (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, kTail>
+                   : paired ? (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, false>
+                            : (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, false, false>;
   int rc = ensure_lds(fn, lds);
   if (rc) return rc;
-  if (paired)
-    hipLaunchKernelGGL((mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair>), grid, dim3(kMhBlock),
-                       lds, st, a);
+  if (tail)
+    launch_sweep(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, kTail>, grid, dim3(kMhBlock), lds, st, a);
+  else if (paired)
+    launch_sweep(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, false>, grid, dim3(kMhBlock), lds, st, a);
   else
-    hipLaunchKernelGGL((mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, false>), grid, dim3(kMhBlock),
-                       lds, st, a);
+    launch_sweep(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, false, false>, grid, dim3(kMhBlock), lds, st, a);
   return SMCDET_OK;
 }
 
@@ -922,7 +939,7 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
     if (tail->resample_u && tail->resample_method != SMCDET_RESAMPLE_SYSTEMATIC)
       return set_error(SMCDET_EINVAL, "resample_u replays systematic resampling only");
     size_t lds_f = 0;
-    if (tail_fusable(*model, N, S, flags, &lds_f)) {
+    if (!(tail->flags & SMCDET_SMC_TWO_LAUNCH) && tail_fusable(*model, N, S, flags, &lds_f)) {
       TileArgs& ta = a.tail;
       ta.flags = kDoTemper | kDoWeights | (tail->idx ? kDoResample : 0u);
       ta.T = T;
@@ -941,7 +958,7 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
       ta.offset = tail->offset;
       ta.u = tail->resample_u;
       ta.idx = tail->idx;
-      ta.smc_flags = tail->flags;
+      ta.smc_flags = tail->flags & ~SMCDET_SMC_TWO_LAUNCH;
       ta.fin_iter = tail->finished_iter;
       ta.iter = tail->iter;
       ta.live = tail->live;
@@ -965,12 +982,13 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
   rc = check_launch("smcdet_mh_sweep");
   if (rc || !split_tail) return rc;
   float* temp = const_cast<float*>(temperature);
+  const uint32_t smc_flags = tail->flags & ~SMCDET_SMC_TWO_LAUNCH;
   if (tail->resample_u && tail->idx) {
     rc = smcdet_temper_reweight(loglik_out, temp, tail->temperature_prev,
                                 tail->log_weights_unnorm, tail->weights, tail->ess,
                                 tail->log_norm_const, T, N, tail->ess_threshold,
                                 tail->resample_method, tail->seed, tail->offset, nullptr,
-                                tail->flags, tail->finished_iter, tail->iter, tail->live, go,
+                                smc_flags, tail->finished_iter, tail->iter, tail->live, go,
                                 tail->live_host, stream);
     if (rc) return rc;
     return smcdet_resample_index(tail->weights, T, N, tail->resample_method, tail->seed,
@@ -979,7 +997,7 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
   return smcdet_temper_reweight(loglik_out, temp, tail->temperature_prev, tail->log_weights_unnorm,
                                 tail->weights, tail->ess, tail->log_norm_const, T, N,
                                 tail->ess_threshold, tail->resample_method, tail->seed,
-                                tail->offset, tail->idx, tail->flags, tail->finished_iter,
+                                tail->offset, tail->idx, smc_flags, tail->finished_iter,
                                 tail->iter, tail->live, go, tail->live_host, stream);
 }
 

@@ -45,7 +45,6 @@ class SingleComponentMH(object):
         self.rng = None           # PhiloxStream; SMCsampler installs its own
         self.debug_flags = 0      # SMCDET_MH_ABLATE_* timing diagnostics (never for sampling)
         self.last_loglik = None   # log-likelihood of the state returned by run()
-        self.launch_events = None  # list -> (start, end) HIP events of each sweep launch
         self._acc_ws = {}
 
     @staticmethod
@@ -176,10 +175,6 @@ class SingleComponentMH(object):
                 raise ValueError("the fused SMC step needs want_loglik=True")
             entry = "smcdet_mh_sweep_step"
             extra = extra + [_hip.ref(tail)]
-        ev = self.launch_events
-        if ev is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(torch.cuda.current_stream(dev))
         _hip.check(getattr(_hip.lib(), entry)(
             _hip.ref(cm), _hip.ref(cp), _hip.ref(ch), _hip.ptr(data), _hip.ptr(temperature),
             T, N, S, anc_p, _hip.ptr(counts), _hip.ptr(locs), _hip.ptr(fluxes),
@@ -189,9 +184,6 @@ class SingleComponentMH(object):
             self.rng.seed, off,
             _hip.ref(rp) if rp is not None else None, flags, _hip.ptr(ll), _hip.ptr(acc),
             _hip.ptr(acc_ws), _hip.ptr(go), *extra, _hip.stream_of(locs)), entry)
-        if ev is not None:
-            e1.record(torch.cuda.current_stream(dev))
-            ev.append((e0, e1))
         del keep
         self.last_loglik = ll
         self.last_counts = counts_out if counts_out is not None else counts
