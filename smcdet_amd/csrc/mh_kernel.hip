@@ -41,7 +41,6 @@
 
 namespace smcdet {
 
-SMCDET_TRACE_TABLE
 SMCDET_WAVE_TABLE
 
 constexpr int kMhWaves = 4;
@@ -592,55 +591,94 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
       using Zero = std::false_type;
       using I2 = std::integral_constant<int, 2>;
       using I3 = std::integral_constant<int, 3>;
+      using I4 = std::integral_constant<int, 4>;
       using I5 = std::integral_constant<int, 5>;
       using I8 = std::integral_constant<int, kSlots>;
       using Win = std::true_type;
       using Same = std::false_type;
-      float dsum = 0.f;
+      // The union-window positions beyond the register slots (a jump of
+      // several px; rare): their delta (WRITE = false) or their rate-image
+      // update after an accept (WRITE = true).
+      auto far_positions = [&](auto WRITE) -> float {
+        float acc = 0.f;
+        const float inv_bw = 1.0f / (float)bw;
+        for (int q = kSlots * kWave + lane; q < npos; q += kWave) {
+          const int aa = (int)(((float)q + 0.5f) * inv_bw);
+          const int bb = q - (int)__umul24((unsigned)aa, (unsigned)bw);
+          const int ph = r0 + aa, pw = c0 + bb;
+          const int p = (int)__umul24((unsigned)ph, (unsigned)m.W) + pw;
+          float lnew;
+          acc += position_delta<MODEL, true>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o, amp_n,
+                                             ao_h, ao_w, an_h, an_w, lnew);
+          if constexpr (decltype(WRITE)::value) lam[p] = lnew;
+        }
+        return acc;
+      };
+      // Reduction, accept decision (kernel.py:114-116) and rate-image update,
+      // inlined into each slot variant's own block: the NS slots' new rates
+      // and pixel indices (s_lam / s_pix) die inside it instead of flowing
+      // into a merge point (their phi copies cost ~16 VALU moves per
+      // iteration).  log alpha = (Hastings + prior term) + tau * dll,
+      // accepted iff it is >= log U (U <= min(1, exp(log alpha)) for U in
+      // [0, 1); nan rejects).  An edge hit (hast = -inf) never updates the
+      // state (the sweep ends below).
+      auto finish = [&](float dsum, auto NS) {
+        constexpr int ns = decltype(NS)::value;
+        constexpr bool kFar = NSL > 1 && ns >= kSlots;
+        if (kFar && npos > kSlots * kWave) dsum += far_positions(std::false_type{});
+        dll = wave_sum(dsum);
+        accept = __builtin_amdgcn_readfirstlane((fmaf(tau, dll, P.hast) >= log_u) ? 1 : 0);
+        if (accept && P.hast != -INFINITY) {
+#pragma unroll
+          for (int i = 0; i < ns; ++i)
+            if (i < nslots) lam[s_pix[i]] = s_lam[i];
+          if (kFar && npos > kSlots * kWave) (void)far_positions(std::true_type{});
+          wave_sync();
+        }
+      };
       if constexpr (NSL == 1) {
+        // small tiles (latency-bound at 7 waves per SIMD): one reduction and
+        // accept after the merge measured faster (C4 4.95 vs 5.12 ms)
+        float dsum = 0.f;
         if (nslots == 1) dsum = same ? slots(I1{}, Same{}) : slots(I1{}, Win{});
+        dll = wave_sum(dsum);
+        accept = __builtin_amdgcn_readfirstlane((fmaf(tau, dll, P.hast) >= log_u) ? 1 : 0);
       } else if (nslots == 0) {
+        finish(0.f, I0{});
       } else if (PAIRED && nslots == 1) {
-        dsum = same ? pairs(I0{}, One{}, Same{}) : pairs(I0{}, One{}, Win{});
+        if (same) finish(pairs(I0{}, One{}, Same{}), I1{});
+        else finish(pairs(I0{}, One{}, Win{}), I1{});
       } else if (PAIRED && nslots == 2) {
-        dsum = same ? pairs(I1{}, Zero{}, Same{}) : pairs(I1{}, Zero{}, Win{});
+        if (same) finish(pairs(I1{}, Zero{}, Same{}), I2{});
+        else finish(pairs(I1{}, Zero{}, Win{}), I2{});
       } else if (PAIRED && nslots <= 3) {
-        dsum = same ? pairs(I1{}, One{}, Same{}) : pairs(I1{}, One{}, Win{});
+        if (same) finish(pairs(I1{}, One{}, Same{}), I3{});
+        else finish(pairs(I1{}, One{}, Win{}), I3{});
       } else if (PAIRED && nslots <= 4) {
-        dsum = same ? pairs(I2{}, Zero{}, Same{}) : pairs(I2{}, Zero{}, Win{});
+        if (same) finish(pairs(I2{}, Zero{}, Same{}), I4{});
+        else finish(pairs(I2{}, Zero{}, Win{}), I4{});
       } else if (PAIRED && nslots <= 5) {
-        dsum = same ? pairs(I2{}, One{}, Same{}) : pairs(I2{}, One{}, Win{});
+        if (same) finish(pairs(I2{}, One{}, Same{}), I5{});
+        else finish(pairs(I2{}, One{}, Win{}), I5{});
       } else if (PAIRED) {
         // 6 slots (both anchors moved): rare; the scalar form needs fewer
         // registers than three packed pairs
-        dsum = slots(I8{}, Win{});
+        finish(slots(I8{}, Win{}), I8{});
       } else if (nslots <= 3) {
-        dsum = same ? slots(I3{}, Same{}) : slots(I3{}, Win{});
+        if (same) finish(slots(I3{}, Same{}), I3{});
+        else finish(slots(I3{}, Win{}), I3{});
       } else if (nslots <= 5) {
-        dsum = same ? slots(I5{}, Same{}) : slots(I5{}, Win{});
+        if (same) finish(slots(I5{}, Same{}), I5{});
+        else finish(slots(I5{}, Win{}), I5{});
       } else {
-        dsum = slots(I8{}, Win{});
+        finish(slots(I8{}, Win{}), I8{});
       }
-      if (NSL > 1 && nslots > 5) {
-        // rare: a union window larger than the register slots (a jump of several px)
-        if (npos > kSlots * kWave) {
-          const float inv_bw = 1.0f / (float)bw;
-          for (int q = kSlots * kWave + lane; q < npos; q += kWave) {
-            const int aa = (int)(((float)q + 0.5f) * inv_bw);
-            const int bb = q - (int)__umul24((unsigned)aa, (unsigned)bw);
-            const int ph = r0 + aa, pw = c0 + bb;
-            float lnew;
-            dsum += position_delta<MODEL, true>(m, xs, lg, lam, (int)__umul24((unsigned)ph, (unsigned)m.W) + pw, aa, bb, ph, pw,
-                                                P, amp_o, amp_n, ao_h, ao_w, an_h, an_w, lnew);
-          }
-        }
-      }
-      dll = wave_sum(dsum);
     }
-
-    // ---- accept / reject (kernel.py:114-128) ----------------------------------
-    const float loga = fmaf(tau, dll, P.hast);
-    accept = __builtin_amdgcn_readfirstlane((loga >= log_u) ? 1 : 0);
+    if constexpr (FULL) {
+      // ---- accept / reject (kernel.py:114-128) --------------------------------
+      const float loga = fmaf(tau, dll, P.hast);
+      accept = __builtin_amdgcn_readfirstlane((loga >= log_u) ? 1 : 0);
+    }
 #ifdef SMCDET_TRACE
     tr_acc += accept;
 #endif
@@ -658,28 +696,11 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
       if constexpr (FULL) {
         cur_ll = new_ll;
       } else {
-#pragma unroll
-        for (int i = 0; i < NSL; ++i)
-          if (i < nslots) lam[s_pix[i]] = s_lam[i];
-        if (NSL > 1 && npos > kSlots * kWave) {
-          const int flh = readlane(bfl, 3 * b), flw = readlane(bfl, 3 * b + 1);
-          const int fh0 = (int)(int16_t)(flh & 0xffff), fh1 = flh >> 16;
-          const int fw0 = (int)(int16_t)(flw & 0xffff), fw1 = flw >> 16;
-          const int ao_h = fh0 - m.R - r0, ao_w = fw0 - m.R - c0;
-          const int an_h = fh1 - m.R - r0, an_w = fw1 - m.R - c0;
-          const float inv_bw = 1.0f / (float)bw;
-          for (int q = kSlots * kWave + lane; q < npos; q += kWave) {
-            const int aa = (int)(((float)q + 0.5f) * inv_bw);
-            const int bb = q - (int)__umul24((unsigned)aa, (unsigned)bw);
-            const int ph = r0 + aa, pw = c0 + bb;
-            float lnew;
-            (void)position_delta<MODEL, true>(m, xs, lg, lam, (int)__umul24((unsigned)ph, (unsigned)m.W) + pw, aa, bb, ph, pw, P,
-                                              amp_o, amp_n, ao_h, ao_w, an_h, an_w, lnew);
-            lam[(int)__umul24((unsigned)ph, (unsigned)m.W) + pw] = lnew;
-          }
+        if constexpr (NSL == 1) {
+          if (nslots == 1) lam[s_pix[0]] = s_lam[0];
+          wave_sync();
         }
         cur_ll += (double)dll;
-        wave_sync();
       }
       // source j takes the proposal (v_writelane)
       sh = writelane(P.hn, P.j, sh);

@@ -9,7 +9,6 @@
 
 namespace smcdet {
 
-SMCDET_TRACE_TABLE
 
 // One 512-thread workgroup per tile (tile.h: the same work the MH sweep's
 // last workgroup runs when the SMC iteration is fused into one launch).

@@ -27,6 +27,9 @@
 
 namespace smcdet {
 
+// (profiling builds: the phase-timestamp table of the including file)
+SMCDET_TRACE_TABLE
+
 constexpr int kTB = 512;            // virtual threads of the tile layout
 constexpr int kTW = kTB / kWave;    // 8 virtual waves
 constexpr int kMaxPer = 32;         // log-likelihoods per virtual thread
