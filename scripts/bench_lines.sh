@@ -21,6 +21,7 @@ run c4 --workload c4 --no-cpu-baseline
 run c5 --workload c5 --no-cpu-baseline
 run mcmc --workload mcmc
 run mala --kernel mala --no-cpu-baseline
+run agg --workload agg --no-cpu-baseline
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_c4 -o run -- \
   python3 bench.py --workload c4 --no-cpu-baseline --no-full-run > $O/prof_c4.log 2>&1
 echo "prof_c4 rc=$?"
