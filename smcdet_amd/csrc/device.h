@@ -198,6 +198,25 @@ __device__ __forceinline__ float wave_sum(float v) {
   v += dpp_f<0x143, 0xc>(v);
   return readlane(v, 63);
 }
+// two independent wave sums, step by step interleaved (each value gets
+// wave_sum's exact operation sequence; the two DPP chains hide each other's
+// latency on the tile pass's latency-bound path)
+__device__ __forceinline__ void wave_sum2(float& a, float& b) {
+  a += dpp_f<0xb1>(a);
+  b += dpp_f<0xb1>(b);
+  a += dpp_f<0x4e>(a);
+  b += dpp_f<0x4e>(b);
+  a += dpp_f<0x114>(a);
+  b += dpp_f<0x114>(b);
+  a += dpp_f<0x118>(a);
+  b += dpp_f<0x118>(b);
+  a += dpp_f<0x142, 0xa>(a);
+  b += dpp_f<0x142, 0xa>(b);
+  a += dpp_f<0x143, 0xc>(a);
+  b += dpp_f<0x143, 0xc>(b);
+  a = readlane(a, 63);
+  b = readlane(b, 63);
+}
 __device__ __forceinline__ double wave_sum(double v) {
   v += dpp_d<0xb1>(v);
   v += dpp_d<0x4e>(v);

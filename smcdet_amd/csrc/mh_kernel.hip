@@ -462,18 +462,20 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
       b = 0;
       j = readlane(bj, 0);
     }
-    // the batch entry is current (its source was not moved since the batch)
+    // the batch entry is current (its source was not moved since the batch);
+    // its lane base as one SGPR (b's phi may sit in a VGPR)
+    const int b3 = __builtin_amdgcn_readfirstlane(3 * b);
     Proposal P;
     P.j = j;
-    P.h = readlane(bmu, 3 * b);
-    P.w = readlane(bmu, 3 * b + 1);
-    P.hn = readlane(bx, 3 * b);
-    P.wn = readlane(bx, 3 * b + 1);
-    P.fn = readlane(bx, 3 * b + 2);
-    P.hast = readlane(bhs, 3 * b + 2);  // Hastings + prior terms
-    const float log_u = readlane(blu, 3 * b + 2);
+    P.h = readlane(bmu, b3);
+    P.w = readlane(bmu, b3 + 1);
+    P.hn = readlane(bx, b3);
+    P.wn = readlane(bx, b3 + 1);
+    P.fn = readlane(bx, b3 + 2);
+    P.hast = readlane(bhs, b3 + 2);  // Hastings + prior terms
+    const float log_u = readlane(blu, b3 + 2);
     // rate contributions g*f*psf, the psf normalisation folded into the amplitude
-    const float amp_o = readlane(bampo, 3 * b + 2), amp_n = readlane(bampn, 3 * b + 2);
+    const float amp_o = readlane(bampo, b3 + 2), amp_n = readlane(bampn, b3 + 2);
 
     // ---- likelihood difference -----------------------------------------------
     float dll;
@@ -494,7 +496,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
       }
       dll = (float)(new_ll - cur_ll);
     } else {
-      const int flh = readlane(bfl, 3 * b), flw = readlane(bfl, 3 * b + 1);
+      const int flh = readlane(bfl, b3), flw = readlane(bfl, b3 + 1);
       const int fh0 = (int)(int16_t)(flh & 0xffff), fh1 = flh >> 16;
       const int fw0 = (int)(int16_t)(flw & 0xffff), fw1 = flw >> 16;
       r0 = max(min(fh0, fh1) - m.R, 0);
@@ -507,7 +509,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
 #ifdef SMCDET_TRACE
       tr_pos += npos;
 #endif
-      const unsigned magic = (unsigned)readlane((int)bmg, 3 * b + 1);  // q/bw, q < 1024
+      const unsigned magic = (unsigned)readlane((int)bmg, b3 + 1);  // q/bw, q < 1024
       const bool same = (fh0 == fh1) && (fw0 == fw1);
       const int ao_h = fh0 - m.R - r0, ao_w = fw0 - m.R - c0;
       const int an_h = fh1 - m.R - r0, an_w = fw1 - m.R - c0;

@@ -136,7 +136,8 @@ __device__ __forceinline__ void vblock_sum2f(const float (&a)[VLayout<NT>::VPT],
   parity ^= 1;
 #pragma unroll
   for (int h = 0; h < VLayout<NT>::VPT; ++h) {
-    const float x = wave_sum(a[h]), y = wave_sum(b[h]);
+    float x = a[h], y = b[h];
+    wave_sum2(x, y);
     if (lane == 0) {
       r->f2[k][vwave<NT>(h)][0] = x;
       r->f2[k][vwave<NT>(h)][1] = y;
