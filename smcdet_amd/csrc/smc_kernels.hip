@@ -10,15 +10,20 @@
 namespace smcdet {
 
 
-// One 512-thread workgroup per tile (tile.h: the same work the MH sweep's
-// last workgroup runs when the SMC iteration is fused into one launch).
+// One workgroup of kTileNT threads per tile, on tile.h's 512-thread virtual
+// layout (so any kTileNT gives the same results; the MH sweep's fused tail
+// runs the same work on its 256 threads).
+#ifndef SMCDET_TILE_NT
+#define SMCDET_TILE_NT 512
+#endif
+constexpr int kTileNT = SMCDET_TILE_NT;
 template <int PER>
-__global__ __launch_bounds__(kTB) void tile_kernel(TileArgs a) {
+__global__ __launch_bounds__(kTileNT) void tile_kernel(TileArgs a) {
   if (a.go && *a.go == 0) return;  // speculatively enqueued iteration that must not run
   extern __shared__ float buf[];  // N floats: weights / cumsum, then N+1 resample slots
   __shared__ TileRed red;
   const int t = blockIdx.x;
-  tile_work<kTB, PER>(a, t, buf, red, threadIdx.x < kWave ? t : -1);
+  tile_work<kTileNT, PER>(a, t, buf, red, threadIdx.x < kWave ? t : -1);
 }
 
 // gather: thread per (t, n, s)
@@ -331,7 +336,7 @@ static int launch_tile(const TileArgs& a, hipStream_t st) {
   int rc = ensure_lds(fn, lds + sizeof(TileRed));
   if (rc) return rc;
   void* args[] = {const_cast<TileArgs*>(&a)};
-  hipError_t e = hipLaunchKernel(fn, dim3(a.T), dim3(kTB), args, lds, st);
+  hipError_t e = hipLaunchKernel(fn, dim3(a.T), dim3(kTileNT), args, lds, st);
   if (e != hipSuccess) return set_error(SMCDET_EHIP, "tile kernel launch: %s", hipGetErrorString(e));
   return check_launch("smcdet tile kernel");
 }

@@ -90,3 +90,12 @@ def test_build_provenance():
     listed = (srcs + " " + hdrs).split()
     assert [os.path.relpath(p, os.path.dirname(_hip._HERE)) for p in _hip.SOURCES] == listed
     assert _hip.built_hash() == _hip.source_hash()
+
+
+def test_launch_timing_pool_without_gpu():
+    """smcdet_launch_timing: negative sizes are refused, 0 disables (no HIP
+    call), and reading an empty pool reports no timed launches."""
+    L = _hip.lib()
+    assert L.smcdet_launch_timing(-1) == -1
+    assert L.smcdet_launch_timing(0) == 0
+    assert _hip.launch_timing_read(4) == []

@@ -112,3 +112,21 @@ def test_small_tiles_take_the_two_launch_path():
     assert _hip.lib().smcdet_mh_sweep_step_fused(_hip.ref(a.ImageModel._cmodel()), 1024, 10, 0) == 0
     b = _sampler(img, 8, 1024, 10, 30, 3, fused_step=False)
     _assert_same(_steps(a, 4), _steps(b, 4))
+
+
+def test_launch_timing_on_dispatch_events():
+    """smcdet_launch_timing (bench.py's kernel time): each timed sweep launch
+    of the two-launch step gets its own positive duration, the pool stops at
+    its size, and timing leaves the results unchanged."""
+    from smcdet_amd import _hip
+    img = _image(32, 5)
+    a = _sampler(img, 32, 1024, 10, 50, 77, fused_step=False)
+    b = _sampler(img, 32, 1024, 10, 50, 77, fused_step=False)
+    _hip.launch_timing(2)
+    try:
+        ta = _steps(a, 3)
+        ms = _hip.launch_timing_read(3)
+    finally:
+        _hip.launch_timing(0)
+    assert len(ms) == 2 and all(0.0 < x < 1000.0 for x in ms)
+    _assert_same(ta, _steps(b, 3))
