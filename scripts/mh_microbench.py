@@ -36,6 +36,9 @@ def main():
     # streams still time the MH sweep on identical states (scripts/ab_kernel.sh)
     ap.add_argument("--state", choices=["torch", "device"], default="torch")
     ap.add_argument("--warm", type=int, default=3, help="MH sweeps before timing (torch state)")
+    # start every sweep from persisted rate images (as SMCsampler does) instead
+    # of an initial render of all sources
+    ap.add_argument("--persist", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -133,10 +136,19 @@ def main():
         "resample_only": lambda: _hip.check(_hip.lib().smcdet_resample_index(
             _hip.ptr(W), T, Np, 1, 1, 0, None, _hip.ptr(idx), _hip.stream_of(ll)), "r"),
     }
+    rates = {}
+    if a.persist:
+        # rate images of (locs, fluxes); every timed sweep reads them (and
+        # writes a second buffer) without moving the state it started from
+        r_in = torch.empty(nt, nt, Np, H * H, device=dev)
+        r_out = torch.empty_like(r_in)
+        p_m71_mh(0).run(img, counts, locs, fluxes, tau, prior=prior, image_model=model,
+                        rate_out=r_in)
+        rates = {"rate_in": r_in, "rate_out": r_out}
     for r in range(a.rounds + 1):
         for k, mh in mhs.items():
             v = timeit(lambda: mh.run(img, counts, locs, fluxes, tau, prior=prior,
-                                      image_model=model))
+                                      image_model=model, **rates))
             if r:
                 times[k].append(v)
         for k, fn in extra.items():
