@@ -50,11 +50,9 @@ def main():
     out = {}
     for i in range(steps):
         idx, s._pending_idx = s._pending_idx, None
-        s.mutate(ancestors=idx)
+        s._step(idx)  # (two launches: the sweep, then the tile kernel)
         torch.cuda.synchronize()
         mh_d = read("smcdet_trace_read_mh", 6)
-        s._temper_reweight(with_resample=True)
-        torch.cuda.synchronize()
         tile_d = read("smcdet_trace_read_tile", 10)[:1]
         out[f"step{i}"] = {
             "tau": float(s.temperature.min()),
@@ -68,7 +66,7 @@ def main():
     fn = _hip.lib().smcdet_trace_read_waves
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
     idx, s._pending_idx = s._pending_idx, None
-    s.mutate(ancestors=idx)
+    s._step(idx)
     torch.cuda.synchronize()
     assert fn(ctypes.addressof(buf), 8192 * 8) == 0
     w = np.frombuffer(buf, dtype=np.uint64).reshape(8192, 8)[:Np].astype(np.float64)
