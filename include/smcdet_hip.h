@@ -153,7 +153,9 @@ int smcdet_host_free(void* host);
  * packet (and no launch bubble) between kernels.  max_launches = 0 disables
  * timing and frees the pool; a new call discards earlier timings.
  * smcdet_launch_timing_read waits for the timed launches and writes the first
- * min(max, *n_out) durations in ms; *n_out = launches timed since enabling. */
+ * min(max, *n_out) durations in ms; *n_out = launches timed since enabling.
+ * The pool is process-global and not thread-safe: enable, launch and read
+ * from one host thread (bench.py does). */
 int smcdet_launch_timing(int32_t max_launches);
 int smcdet_launch_timing_read(float* ms, int32_t max, int32_t* n_out);
 
