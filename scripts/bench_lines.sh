@@ -17,6 +17,7 @@ run() {  # $1 = name, rest = bench args
 }
 run c2
 run c3_64tiles --total-tiles 64 --no-cpu-baseline
+run c3_9tiles --tiles-per-gpu 9 --no-cpu-baseline --no-vs-ref  # ~ a C3 rank share (64 tiles / 8 GPUs), square grid
 run c4 --workload c4 --no-cpu-baseline
 run c5 --workload c5 --no-cpu-baseline
 run mcmc --workload mcmc
