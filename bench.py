@@ -44,6 +44,7 @@ M71 = dict(flux_alpha=0.21411753249015655, flux_lower=0.06291294097900389,
 COUNTS_RATE_C2 = 5.0 / (40 * 40)
 M71_COUNTS_RATE = 0.030264640226960182  # notebooks/smc.ipynb cell 2
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md (spec)
+C3_TILES = 64               # BASELINE configs[2]: 64 32x32 tiles over the node
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md (vector FP32, spec)
 B_ALG_PER_STEP = 248        # SURVEY §8d, S=10
 F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
@@ -99,6 +100,8 @@ def parse():
     # no kernel-timing pass after the timed region (the roofline then uses the
     # step time as the kernel time)
     ap.add_argument("--no-kernel-timing", action="store_true")
+    # skip the C3 strong-scaling leg (c3_leg) of the default C2 run
+    ap.add_argument("--no-c3", action="store_true")
     return ap.parse_args()
 
 
@@ -538,6 +541,53 @@ def _full_run(s2):
     return time.perf_counter() - t0
 
 
+def c3_leg(args, dev, rank, world, dist, backend):
+    """BASELINE configs[2] (C3) riding along the default C2 run: the 64 32x32
+    tiles split contiguously over the ranks (--total-tiles 64 semantics: tile
+    g drawn from seed 1000 + g whatever the rank count), timed like the main
+    line (warmup, barrier + synchronize on both sides, MAX over ranks).  Every
+    rank runs it, so the driver's N = 1, 2, 4, 8 runs of the default command
+    measure C3's strong scaling too.  The value is the whole job's
+    particle-steps/s."""
+    import argparse as _ap
+    import torch.distributed as tdist
+    a3 = _ap.Namespace(**vars(args))
+    a3.total_tiles, a3.tiles_per_gpu = C3_TILES, 1
+    s, _, _, _, cfg = build_sampler(a3, dev, rank)
+    s.fused_step = False
+    s.initialize()
+    s._temper_reweight(with_resample=True)
+
+    def step():
+        idx, s._pending_idx = s._pending_idx, None
+        s._step(idx)
+
+    steps = max(3, min(args.steps, 10))
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu",
+                         dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t)
+    value = C3_TILES * args.particles * args.mh_iters * steps / elapsed
+    return {"metric": f"particle-steps/sec (C3: {C3_TILES} x 32x32 tiles, 4096 particles)",
+            "value": value, "unit": "particle-steps/sec", "n_gpus": world, "steps": steps,
+            "warmup": 2, "ms_per_step": elapsed / steps * 1e3, "scaling": "strong",
+            "config": {"workload": cfg["workload"], "tiles_per_gpu_rank0": cfg["tiles_per_gpu"]}}
+
+
 def _hip_fused(s):
     """Whether smcdet_mh_sweep_step runs this sampler's shapes as one launch."""
     from smcdet_amd import _hip
@@ -628,6 +678,10 @@ def main():
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t)
     mh_ms = sum(ev) / max(len(ev), 1)
+    c3 = None
+    if (args.workload == "c2" and args.kernel == "mh" and args.total_tiles == 0
+            and args.tiles_per_gpu == 1 and not args.no_c3 and world <= C3_TILES):
+        c3 = c3_leg(args, dev, rank, world, dist, backend)
 
     if args.total_tiles > 0:  # strong scaling: every rank's tiles, uneven shares included
         value = args.total_tiles * args.particles * args.mh_iters * args.steps / elapsed
@@ -682,6 +736,8 @@ def main():
                 "acc_rate": float(s.mutation_acc_rates.mean()),
                 "ess_mean": float(s.ess.mean())},
     }
+    if c3 is not None:
+        out["c3_strong"] = c3
     # SURVEY §8d also asks for the wall time to temperature 1: one complete
     # run() (initialise, SMC loop with its per-iteration stopping check, final
     # resample, prune) on a fresh sampler, outside the timed region
