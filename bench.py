@@ -48,8 +48,8 @@ C3_TILES = 64               # BASELINE configs[2]: 64 32x32 tiles over the node
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md (vector FP32, spec)
 B_ALG_PER_STEP = 248        # SURVEY §8d, S=10
 F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
-PMC_FILE = "pmc_mh_r02s3.json"  # rocprofv3 FETCH_SIZE+WRITE_SIZE per MH launch (scripts/profile.sh)
-PMC_VALU_FILE = "pmc_valu_mh_r02s3.json"  # rocprofv3 SQ VALU counts per MH launch (scripts/profile.sh)
+PMC_FILE = "pmc_mh_r02s4.json"  # rocprofv3 FETCH_SIZE+WRITE_SIZE per MH launch (scripts/profile.sh)
+PMC_VALU_FILE = "pmc_valu_mh_r02s4.json"  # rocprofv3 SQ VALU counts per MH launch (scripts/profile.sh)
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions/s: 1 per SIMD per 4 cycles (measured 4.2)
 # the reference itself (torch CPU, smcdet/kernel.py) on the same workload, SURVEY §6 (build
 # container, 8 cores; the reference does not travel to the GPU box)
