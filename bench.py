@@ -12,7 +12,9 @@ log-likelihood) and the per-tile temper + reweight + resampling-index launch.
 particle-steps per step = N * 100 per tile.  Multi-GPU: one process per GPU,
 each rank owns its own tile(s) (weak scaling, no data-path collective); the
 timed region is bracketed by barrier + synchronize and the MAX over ranks is
-reported.  value = all ranks' particle-steps / that time.
+reported.  value = all ranks' particle-steps / that time.  The default run
+also times BASELINE configs[2] (C3: 64 tiles split over the ranks, strong
+scaling) with the same bracket and reports it as `c3_strong` (--no-c3 skips).
 
 Roofline objects: `roofline` (HBM, as BASELINE.json asks): algorithmic bytes
 of the MH launch = 248 B per particle-step (state read+write
