@@ -53,6 +53,10 @@ F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
 PMC_FILE = "pmc_mh_r02s4.json"  # rocprofv3 FETCH_SIZE+WRITE_SIZE per MH launch (scripts/profile.sh)
 PMC_VALU_FILE = "pmc_valu_mh_r02s4.json"  # rocprofv3 SQ VALU counts per MH launch (scripts/profile.sh)
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions/s: 1 per SIMD per 4 cycles (measured 4.2)
+# measured SIMD issue cycles per wave-instruction (scripts/probe/isa_probe.hip, 4 waves/SIMD,
+# profiles/r01_s2_isa_probe.txt): plain VALU 4.2, transcendental 8.6, packed f32 6.0
+ISSUE_CYC_VALU, ISSUE_CYC_TRANS = 4.2, 8.6
+SIMD_CYCLES_PER_S = 256 * 4 * 2.4e9
 # the reference itself (torch CPU, smcdet/kernel.py) on the same workload, SURVEY §6 (build
 # container, 8 cores; the reference does not travel to the GPU box)
 REFERENCE_CPU = {"value": 8466.0, "unit": "particle-steps/sec", "cores": 8, "kind": "reference",
@@ -464,6 +468,16 @@ def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
                 "valu_issue_frac": insts / t / VALU_ISSUE_PEAK,
                 "tflops": flops / t / 1e12, "frac": flops / t / 1e12 / FP32_PEAK_TFLOPS,
                 "source": f"profiles/{PMC_VALU_FILE}"}
+            # the instruction mix weighted by its measured issue cost: SIMD
+            # cycles the launch's VALU stream needs per particle-step (a lower
+            # bound: packed ops, 6.0 cycles, are counted as plain ones) against
+            # the SIMD cycles the launch had per particle-step
+            trans = per_step.get("SQ_INSTS_VALU_TRANS_F32") or 0.0
+            cyc = (per_step["SQ_INSTS_VALU"] - trans) * ISSUE_CYC_VALU + trans * ISSUE_CYC_TRANS
+            avail = SIMD_CYCLES_PER_S * t / launch_steps
+            out["executed"]["issue_cycles_per_particle_step"] = cyc
+            out["executed"]["issue_cycles_available"] = avail
+            out["executed"]["issue_cycle_frac"] = cyc / avail
         except Exception as e:  # never fail the bench line on it
             out["executed"] = {"error": repr(e)}
     return out
