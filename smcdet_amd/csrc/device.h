@@ -265,7 +265,7 @@ struct DevModel {
   float g;      // flux -> ADU scale (adu_per_nmgy; 1 for Poisson)
   // M71: psf(r2) = (exp2(k1 r2) + b exp2(k2 r2) + p0 exp2(kb log2(1 + k3 r2))) * inv_norm
   float k1, k2, b, k3, kb, p0, inv_norm;
-  float lb2, lp02;  // log2(b), log2(p0): b and p0 folded into the exponents
+  float lb2, lp02;  // log2(b), log2(p0): b and p0 folded into the exponents (mcmc.h)
   // Poisson (basic) model: psf(r2) = amp * exp2(kg r2)
   float kg, amp;
   // M71 noise: var = s0sq + eta * rate
@@ -282,9 +282,9 @@ template <int MODEL>
 __device__ __forceinline__ float psf_raw(const DevModel& m, float r2) {
   if constexpr (MODEL == SMCDET_MODEL_M71) {
     const float t1 = fast_exp2(m.k1 * r2);
-    const float t2 = fast_exp2(fmaf(m.k2, r2, m.lb2));
-    const float t3 = fast_exp2(fmaf(m.kb, fast_log2(fmaf(m.k3, r2, 1.0f)), m.lp02));
-    return t1 + t2 + t3;
+    const float e2 = fast_exp2(m.k2 * r2);
+    const float e3 = fast_exp2(m.kb * fast_log2(fmaf(m.k3, r2, 1.0f)));
+    return fmaf(m.p0, e3, fmaf(m.b, e2, t1));
   } else {
     return fast_exp2(m.kg * r2);
   }
@@ -366,10 +366,13 @@ __device__ __forceinline__ f2 rcp2(f2 x) { return f2{fast_rcp(x.x), fast_rcp(x.y
 template <int MODEL>
 __device__ __forceinline__ f2 psf_raw2(const DevModel& m, f2 r2) {
   if constexpr (MODEL == SMCDET_MODEL_M71) {
+    // b and p0 as multipliers (b e2 + t1, then p0 e3 + that): every packed
+    // op then has one scalar operand (VOP3P reads one SGPR; a second one
+    // would be copied into a VGPR pair each iteration)
     const f2 t1 = exp2_2(m.k1 * r2);
-    const f2 t2 = exp2_2(fma2(r2, m.k2, m.lb2));
-    const f2 t3 = exp2_2(fma2(log2_2(fma2(r2, m.k3, 1.0f)), m.kb, m.lp02));
-    return t1 + t2 + t3;
+    const f2 e2 = exp2_2(m.k2 * r2);
+    const f2 e3 = exp2_2(m.kb * log2_2(fma2(r2, m.k3, 1.0f)));
+    return fma2(e3, m.p0, fma2(e2, m.b, t1));
   } else {
     return exp2_2(m.kg * r2);
   }
