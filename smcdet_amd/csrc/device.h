@@ -171,8 +171,12 @@ __device__ __forceinline__ float writelane(float x, int lane, float v) {
 
 // 64-lane reductions on DPP (no LDS crossbar round trips): quad_perm
 // [1,0,3,2], [2,3,0,1], row_shr:4, row_shr:8 leave each row's sum in its lane
-// 15; row_bcast:15 (rows 1,3) and row_bcast:31 (rows 2,3) fold the rows into
-// lane 63, which is broadcast with v_readlane.  Call from converged code.
+// 15; row_bcast:15 and row_bcast:31 fold the rows into lane 63, which is
+// broadcast with v_readlane.  Call from converged code.  The two broadcast
+// steps write every row (bound_ctrl: rows without a source add 0): lane 63
+// gets the same (R3 + R2) + (R1 + R0) as with the rows 1,3 / 2,3 masks, and
+// the compiler fuses each step into one v_add_f32_dpp (the masked form needs
+// a zeroed `old` register and a separate v_mov_b32_dpp).
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ int dpp_move(int v) {
   return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xf, false);
@@ -180,6 +184,10 @@ __device__ __forceinline__ int dpp_move(int v) {
 template <int CTRL, int ROW_MASK = 0xf>
 __device__ __forceinline__ float dpp_f(float v) {
   return __int_as_float(dpp_move<CTRL, ROW_MASK>(__float_as_int(v)));
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f_bc(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, true));
 }
 template <int CTRL, int ROW_MASK = 0xf>
 __device__ __forceinline__ double dpp_d(double v) {
@@ -194,8 +202,8 @@ __device__ __forceinline__ float wave_sum(float v) {
   v += dpp_f<0x4e>(v);
   v += dpp_f<0x114>(v);
   v += dpp_f<0x118>(v);
-  v += dpp_f<0x142, 0xa>(v);
-  v += dpp_f<0x143, 0xc>(v);
+  v += dpp_f_bc<0x142>(v);
+  v += dpp_f_bc<0x143>(v);
   return readlane(v, 63);
 }
 // two independent wave sums, step by step interleaved (each value gets
@@ -210,10 +218,10 @@ __device__ __forceinline__ void wave_sum2(float& a, float& b) {
   b += dpp_f<0x114>(b);
   a += dpp_f<0x118>(a);
   b += dpp_f<0x118>(b);
-  a += dpp_f<0x142, 0xa>(a);
-  b += dpp_f<0x142, 0xa>(b);
-  a += dpp_f<0x143, 0xc>(a);
-  b += dpp_f<0x143, 0xc>(b);
+  a += dpp_f_bc<0x142>(a);
+  b += dpp_f_bc<0x142>(b);
+  a += dpp_f_bc<0x143>(a);
+  b += dpp_f_bc<0x143>(b);
   a = readlane(a, 63);
   b = readlane(b, 63);
 }
