@@ -50,8 +50,8 @@ C3_TILES = 64               # BASELINE configs[2]: 64 32x32 tiles over the node
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md (vector FP32, spec)
 B_ALG_PER_STEP = 248        # SURVEY §8d, S=10
 F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
-PMC_FILE = "pmc_mh_r02s4.json"  # rocprofv3 FETCH_SIZE+WRITE_SIZE per MH launch (scripts/profile.sh)
-PMC_VALU_FILE = "pmc_valu_mh_r02s4.json"  # rocprofv3 SQ VALU counts per MH launch (scripts/profile.sh)
+PMC_FILE = "pmc_mh_r02s4b.json"  # rocprofv3 FETCH_SIZE+WRITE_SIZE per MH launch (scripts/profile.sh)
+PMC_VALU_FILE = "pmc_valu_mh_r02s4b.json"  # rocprofv3 SQ VALU counts per MH launch (scripts/profile.sh)
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions/s: 1 per SIMD per 4 cycles (measured 4.2)
 # measured SIMD issue cycles per wave-instruction (scripts/probe/isa_probe.hip, 4 waves/SIMD,
 # profiles/r01_s2_isa_probe.txt): plain VALU 4.2, transcendental 8.6, packed f32 6.0
