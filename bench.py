@@ -50,8 +50,10 @@ C3_TILES = 64               # BASELINE configs[2]: 64 32x32 tiles over the node
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md (vector FP32, spec)
 B_ALG_PER_STEP = 248        # SURVEY §8d, S=10
 F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
-PMC_FILE = "pmc_mh_r02s4b.json"  # rocprofv3 FETCH_SIZE+WRITE_SIZE per MH launch (scripts/profile.sh)
-PMC_VALU_FILE = "pmc_valu_mh_r02s4b.json"  # rocprofv3 SQ VALU counts per MH launch (scripts/profile.sh)
+# rocprofv3 PMC summary of the C2 MH launch (scripts/profile.sh + scripts/pmc_summary.py):
+# FETCH_SIZE / WRITE_SIZE (HBM traffic), SQ VALU counts, GRBM_GUI_ACTIVE (effective clock),
+# and the sha1 of the library sources it was measured on
+PMC_FILE = "pmc_mh_r03.json"
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions/s: 1 per SIMD per 4 cycles (measured 4.2)
 # measured SIMD issue cycles per wave-instruction (scripts/probe/isa_probe.hip, 4 waves/SIMD,
 # profiles/r01_s2_isa_probe.txt): plain VALU 4.2, transcendental 8.6, packed f32 6.0
@@ -108,6 +110,8 @@ def parse():
     ap.add_argument("--no-kernel-timing", action="store_true")
     # skip the C3 strong-scaling leg (c3_leg) of the default C2 run
     ap.add_argument("--no-c3", action="store_true")
+    # skip the untimed step-spread passes
+    ap.add_argument("--no-spread", action="store_true")
     return ap.parse_args()
 
 
@@ -436,6 +440,27 @@ def bench_mcmc(args, dev, rank, world):
     }
 
 
+def pmc_summary(args):
+    """The committed PMC summary of the C2 MH launch, or (None, reason).  A
+    summary measured on other library sources than the loaded library's is
+    stale: its counters do not describe this run's kernel."""
+    if args.workload != "c2" or args.kernel != "mh" or args.full_recompute:
+        return None, "no PMC summary for this workload"
+    path = os.path.join(ROOT, "profiles", PMC_FILE)
+    if not os.path.exists(path):
+        return None, f"profiles/{PMC_FILE} missing"
+    try:
+        d = json.load(open(path))
+    except Exception as e:  # never fail the bench line on it
+        return None, repr(e)
+    from smcdet_amd import _hip
+    built = _hip.built_hash()
+    if d.get("source_hash") != built:
+        return None, (f"stale: profiles/{PMC_FILE} was measured on library sources "
+                      f"{d.get('source_hash')}, this library is {built}")
+    return d, f"profiles/{PMC_FILE}"
+
+
 def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
     """The binding resource (FP32 VALU issue).  reference_equivalent: SURVEY
     §8d's FLOPs of the reference's full re-render per particle-step, which the
@@ -449,11 +474,11 @@ def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
                "alg_flop_per_particle_step": f_alg,
                "tflops": mh_rate * f_alg / 1e12, "peak_fp32_tflops": FP32_PEAK_TFLOPS,
                "frac": mh_rate * f_alg / 1e12 / FP32_PEAK_TFLOPS}}
-    pmc = os.path.join(ROOT, "profiles", PMC_VALU_FILE)
-    if (os.path.exists(pmc) and args.workload == "c2" and args.kernel == "mh"
-            and not args.full_recompute):
+    d, src = pmc_summary(args)
+    if d is None:
+        out["executed"] = {"omitted": src}
+    else:
         try:
-            d = json.load(open(pmc))
             per_step = d["per_particle_step"]
             insts = per_step["SQ_INSTS_VALU"] * launch_steps     # wave-instructions per launch
             # SQ_INSTS_VALU_FLOPS_FP32(_TRANS) count FLOPs per wave-instruction
@@ -467,7 +492,7 @@ def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
                 "valu_issue_rate": insts / t, "valu_issue_peak": VALU_ISSUE_PEAK,
                 "valu_issue_frac": insts / t / VALU_ISSUE_PEAK,
                 "tflops": flops / t / 1e12, "frac": flops / t / 1e12 / FP32_PEAK_TFLOPS,
-                "source": f"profiles/{PMC_VALU_FILE}"}
+                "source": src, "source_hash": d.get("source_hash")}
             # the instruction mix weighted by its measured issue cost: SIMD
             # cycles the launch's VALU stream needs per particle-step (a lower
             # bound: packed ops, 6.0 cycles, are counted as plain ones) against
@@ -478,6 +503,20 @@ def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
             out["executed"]["issue_cycles_per_particle_step"] = cyc
             out["executed"]["issue_cycles_available"] = avail
             out["executed"]["issue_cycle_frac"] = cyc / avail
+            # the same at the clock the launch actually ran at: GRBM_GUI_ACTIVE
+            # / 8 XCDs / the profiled launch's duration (MI355X_MICROARCH.md,
+            # "DVFS give-back"); the profiled pass's own cycles per particle-step
+            # need no clock at all
+            clk = d.get("effective_clock")
+            if clk:
+                ghz = clk["ghz"]
+                avail_eff = 256 * 4 * ghz * 1e9 * t / launch_steps
+                out["executed"]["effective_clock_ghz"] = ghz
+                out["executed"]["issue_cycles_available_at_effective_clock"] = avail_eff
+                out["executed"]["issue_cycle_frac_at_effective_clock"] = cyc / avail_eff
+                out["executed"]["issue_cycle_frac_profiled_launch"] = (
+                    cyc * launch_steps / (256 * 4 * clk["cycles_per_xcd"]))
+                out["executed"]["effective_clock_source"] = clk.get("note")
         except Exception as e:  # never fail the bench line on it
             out["executed"] = {"error": repr(e)}
     return out
@@ -486,7 +525,7 @@ def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
 def vs_reference(dev, which="c2_moderate", n_runs=48):
     """North-star parity at the headline geometry, outside the timed region:
     the reference's recorded runs (tests/golden/stats_<which>.json: one 32x32
-    M71 tile, S=10, N=512, K=20, systematic, >= 24 seeds) against n_runs runs
+    M71 tile, S=10, N=4096 or 512, K=20, systematic, >= 20 seeds) against n_runs runs
     of this sampler on the same image -- one launch grid of n_runs independent
     copies of the tile (independent stopping = one single-tile run per copy,
     each with its own Philox streams).  Means and standard errors of log Z,
@@ -598,10 +637,44 @@ def c3_leg(args, dev, rank, world, dist, backend):
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t)
     value = C3_TILES * args.particles * args.mh_iters * steps / elapsed
+    gather = catalog_gather(s, rank, world, dist, backend) if dist else None
     return {"metric": f"particle-steps/sec (C3: {C3_TILES} x 32x32 tiles, 4096 particles)",
             "value": value, "unit": "particle-steps/sec", "n_gpus": world, "steps": steps,
             "warmup": 2, "ms_per_step": elapsed / steps * 1e3, "scaling": "strong",
-            "config": {"workload": cfg["workload"], "tiles_per_gpu_rank0": cfg["tiles_per_gpu"]}}
+            "config": {"workload": cfg["workload"], "tiles_per_gpu_rank0": cfg["tiles_per_gpu"]},
+            "catalog_gather": gather}
+
+
+def catalog_gather(s, rank, world, dist, backend):
+    """north_star's one collective: the end-of-run catalog gather of every
+    rank's tiles (smcdet_amd.distributed.gather_tile_results: one gather to
+    rank 0 per field, RCCL over xGMI for device tensors), timed after the C3
+    leg with barrier + synchronize on both sides, MAX over ranks."""
+    import torch.distributed as tdist
+    from smcdet_amd.distributed import gather_tile_results
+    T = s._T
+    local = {"counts": s.counts.reshape(T, -1), "locs": s.locs.reshape(T, *s.locs.shape[2:]),
+             "fluxes": s.fluxes.reshape(T, *s.fluxes.shape[2:]),
+             "weights": s.weights.reshape(T, -1),
+             "log_normalizing_constant": s.log_normalizing_constant.reshape(T),
+             "ess": s.ess.reshape(T)}
+    nbytes = sum(v.numel() * v.element_size() for v in local.values())
+    gather_tile_results(local, C3_TILES, 8, rank, world)  # warm-up (communicator setup)
+    torch.cuda.synchronize()
+    tdist.barrier()
+    t0 = time.perf_counter()
+    out = gather_tile_results(local, C3_TILES, 8, rank, world)
+    torch.cuda.synchronize()
+    tdist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=s.device if backend == "nccl" else "cpu", dtype=torch.float64)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    res = {"backend": backend, "ms": float(t) * 1e3, "bytes_per_rank": nbytes,
+           "fields": sorted(local)}
+    if rank == 0:
+        res["gathered_shape_locs"] = list(out["locs"].shape)
+        res["gathered_device"] = str(out["locs"].device)
+    return res
 
 
 def _hip_fused(s):
@@ -620,7 +693,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("SMCDET_DIST_BACKEND", "nccl") != "nccl":
         local %= max(torch.cuda.device_count(), 1)  # rehearsal: ranks may share a GPU
-    dist = world > 1
+    # a process group whenever torchrun launched us -- also at world size 1
+    # (the driver's N = 1 SCALE run), so its barriers, MAX-over-ranks and the
+    # catalog gather run through the same RCCL path as N = 2, 4, 8
+    dist = world > 1 or ("MASTER_ADDR" in os.environ and "RANK" in os.environ)
     # backend "nccl" (= RCCL on ROCm) for the driver's multi-GPU runs;
     # SMCDET_DIST_BACKEND=gloo rehearses the same code path with several ranks
     # sharing one GPU (RCCL refuses two ranks on one device)
@@ -679,6 +755,7 @@ def main():
     # leaves a 7-10 us bubble before the next launch (rocprofv3 kernel traces,
     # profiles/r02_s3_gap_bench.txt), while untimed back-to-back launches run
     # gap-free.
+    starts = []
     if args.no_kernel_timing:
         ev = [elapsed * 1e3 / args.steps]
     else:
@@ -687,7 +764,18 @@ def main():
             step()
         torch.cuda.synchronize()
         ev = _hip.launch_timing_read(args.steps)
+        starts = _hip.launch_timing_starts(args.steps)
         _hip.launch_timing(0)
+    # step-time spread (untimed): the same steps in 3 more bracketed passes,
+    # and the launch-to-launch intervals of the timing pass above
+    passes = []
+    for _ in range(0 if args.no_spread else 3):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        passes.append((time.perf_counter() - t1) / args.steps * 1e3)
     if dist:
         t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu",
                          dtype=torch.float64)
@@ -715,14 +803,8 @@ def main():
         f_alg *= 3
     achieved_gbs = b_alg * launch_steps / (mh_ms * 1e-3) / 1e9
     mh_rate = launch_steps / (mh_ms * 1e-3)
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", PMC_FILE)
-    if (os.path.exists(pmc) and args.workload == "c2" and not args.full_recompute
-            and args.kernel == "mh"):
-        try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    pmc, _ = pmc_summary(args)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     out = {
         "metric": ("particle-steps/sec (4096 particles, 32x32 tile)"
                    if args.workload == "c2" and args.kernel == "mh"
@@ -752,6 +834,22 @@ def main():
                 "acc_rate": float(s.mutation_acc_rates.mean()),
                 "ess_mean": float(s.ess.mean())},
     }
+    def pct(v):
+        import numpy as np
+        if len(v) == 0:
+            return None
+        a = np.asarray(v, dtype=np.float64)
+        return {"min": float(a.min()), "p50": float(np.percentile(a, 50)),
+                "p90": float(np.percentile(a, 90)), "max": float(a.max()), "n": int(a.size)}
+
+    import numpy as _np
+    out["step_spread"] = {
+        "timed_ms_per_step": elapsed / args.steps * 1e3,
+        "repeat_passes_ms_per_step": passes,
+        "launch_interval_ms": pct(_np.diff(starts)) if len(starts) > 1 else None,
+        "kernel_ms": pct(ev),
+        "note": "untimed: 3 more bracketed passes of the same steps; sweep-launch start-to-start "
+                "intervals and durations from the dispatch-stamped timing pass"}
     if c3 is not None:
         out["c3_strong"] = c3
     # SURVEY §8d also asks for the wall time to temperature 1: one complete
@@ -767,10 +865,16 @@ def main():
                                      "ms_per_iteration": run_s / max(int(s2.iter), 1) * 1e3,
                                      "temperature_min": float(s2.temperature.min())}
     if rank == 0 and args.workload == "c2" and args.kernel == "mh" and not args.no_vs_ref:
-        try:
-            out["smc"]["vs_reference"] = vs_reference(dev)
-        except Exception as e:  # report, never fail the bench line on it
-            out["smc"]["vs_reference"] = {"error": repr(e)}
+        # the headline particle count first (N = 4096, tests/golden/
+        # stats_c2_moderate_4096.json), then the reduced-N target
+        for key, which in (("vs_reference", "c2_moderate_4096"),
+                           ("vs_reference_n512", "c2_moderate")):
+            try:
+                r = vs_reference(dev, which)
+            except Exception as e:  # report, never fail the bench line on it
+                r = {"error": repr(e)}
+            if r is not None:
+                out["smc"][key] = r
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
         try:
             out["cpu_baseline"] = cpu_baseline(args, cpu_tile.cpu().numpy(),

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 14
+#define SMCDET_ABI_VERSION 15
 
 /* status codes */
 #define SMCDET_OK 0
@@ -125,12 +125,20 @@ typedef struct smcdet_mh {
 
 /* Optional replay of recorded draws (tests): per MH iteration k, tile t,
  * particle n: the chosen component, the two location uniforms and the flux
- * uniform of the chosen component, and the accept uniform. */
+ * uniform of the chosen component, and the accept uniform.
+ * trace_loga / trace_accept (nullable; smcdet_mh_sweep / _step only): the
+ * sweep writes each decision's log alpha (float32, as the kernel evaluated
+ * it) and its accept flag (0/1) at [k,t,n] -- decision-by-decision parity
+ * against recorded reference decisions (kernel.py:114-116).  Iterations a
+ * particle does not run (after an upper-edge freeze, or K = 0) are left
+ * untouched.  Only the replay instantiation carries these stores. */
 typedef struct smcdet_mh_replay {
   const int32_t* comp; /* [K,T,N]   */
   const float* uloc;   /* [K,T,N,2] */
   const float* uflux;  /* [K,T,N]   */
   const float* uacc;   /* [K,T,N]   */
+  float* trace_loga;   /* [K,T,N] (nullable) */
+  uint8_t* trace_accept; /* [K,T,N] (nullable) */
 } smcdet_mh_replay_t;
 
 /* "smcdet_hip <version> (gfx950) src <sha1 of the library's sources>" */
@@ -158,6 +166,9 @@ int smcdet_host_free(void* host);
  * from one host thread (bench.py does). */
 int smcdet_launch_timing(int32_t max_launches);
 int smcdet_launch_timing_read(float* ms, int32_t max, int32_t* n_out);
+/* The same launches' start times in ms after the first timed launch's start
+ * (launch-to-launch intervals: the step-time spread bench.py reports). */
+int smcdet_launch_timing_starts(float* ms, int32_t max, int32_t* n_out);
 
 /* ImageModel.loglikelihood / M71ImageModel.loglikelihood
  * (smcdet/images.py:85-102, :159-175): out[T,N]. */

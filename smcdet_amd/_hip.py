@@ -23,7 +23,7 @@ SMCDET_RESAMPLE_SYSTEMATIC = 1
 SMCDET_MH_FULL_RECOMPUTE = 1
 SMCDET_MH_COMPONENT_BY_COUNT = 2
 SMCDET_MH_SKIP_DONE = 4
-ABI_VERSION = 14
+ABI_VERSION = 15
 SMCDET_SMC_FREEZE_DONE = 1
 SMCDET_SMC_TWO_LAUNCH = 2
 
@@ -83,7 +83,10 @@ class MHC(ctypes.Structure):
 
 
 class ReplayC(ctypes.Structure):
-    _fields_ = [("comp", c_p), ("uloc", c_p), ("uflux", c_p), ("uacc", c_p)]
+    """smcdet_mh_replay_t: recorded draws, plus the optional decision trace
+    (log alpha and accept flag per [k, t, n]) the MH sweep writes."""
+    _fields_ = [("comp", c_p), ("uloc", c_p), ("uflux", c_p), ("uacc", c_p),
+                ("trace_loga", c_p), ("trace_accept", c_p)]
 
 
 class SmcTailC(ctypes.Structure):
@@ -103,6 +106,7 @@ _SIGS = {
     "smcdet_host_free": ([c_p], c_i),
     "smcdet_launch_timing": ([c_i], c_i),
     "smcdet_launch_timing_read": ([c_p, c_i, c_p], c_i),
+    "smcdet_launch_timing_starts": ([c_p, c_i, c_p], c_i),
     "smcdet_last_error": ([], ctypes.c_char_p),
     "smcdet_loglik": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
     "smcdet_render": ([c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
@@ -222,6 +226,16 @@ def launch_timing_read(max_launches: int):
     n = c_i(0)
     check(lib().smcdet_launch_timing_read(ctypes.addressof(buf), int(max_launches),
                                           ctypes.byref(n)), "smcdet_launch_timing_read")
+    return [float(buf[i]) for i in range(min(n.value, int(max_launches)))]
+
+
+def launch_timing_starts(max_launches: int):
+    """Start times (ms after the first) of the sweep launches timed since
+    launch_timing()."""
+    buf = (ctypes.c_float * max(int(max_launches), 1))()
+    n = c_i(0)
+    check(lib().smcdet_launch_timing_starts(ctypes.addressof(buf), int(max_launches),
+                                            ctypes.byref(n)), "smcdet_launch_timing_starts")
     return [float(buf[i]) for i in range(min(n.value, int(max_launches)))]
 
 

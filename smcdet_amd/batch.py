@@ -38,6 +38,13 @@ class BatchSMC(object):
             raise ValueError("images must be [B, H, H]")
         self.num_images = images.shape[0]
         B, H, _ = images.shape
+        # every image is a whole image: with pad_mode "partition" each gets the
+        # box of a 1x1 grid (padded on all four sides), not the box of its
+        # column in the [1, B] launch grid
+        if "tile_boxes" not in sampler_kwargs and hasattr(Prior, "tile_boxes"):
+            box = Prior.tile_boxes((1, 1))
+            if box is not None:
+                sampler_kwargs["tile_boxes"] = box.repeat(B, 1)
         self.sampler = SMCsampler.from_tiles(
             images.reshape(1, B, H, H), Prior, ImageModel, MutationKernel, num_catalogs,
             ess_threshold_prop, resample_method, flux_detection_threshold, max_smc_iters,

@@ -169,6 +169,17 @@ int smcdet_launch_timing_read(float* ms, int32_t max, int32_t* n_out) {
   return SMCDET_OK;
 }
 
+int smcdet_launch_timing_starts(float* ms, int32_t max, int32_t* n_out) {
+  const int n = smcdet::g_tused < max ? smcdet::g_tused : max;
+  for (int i = 0; i < n; ++i) {
+    if (hipEventSynchronize(smcdet::g_tev[2 * i]) != hipSuccess ||
+        hipEventElapsedTime(&ms[i], smcdet::g_tev[0], smcdet::g_tev[2 * i]) != hipSuccess)
+      return smcdet::set_error(SMCDET_EHIP, "launch %d: event timing failed", i);
+  }
+  if (n_out) *n_out = smcdet::g_tused;
+  return SMCDET_OK;
+}
+
 #ifndef SMCDET_SRC_HASH
 #define SMCDET_SRC_HASH "unknown"
 #endif

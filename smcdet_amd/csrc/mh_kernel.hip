@@ -81,6 +81,8 @@ struct MhArgs {
   const float* r_uloc;
   const float* r_uflux;
   const float* r_uacc;
+  float* r_loga;                     // replay decision trace [K,T,N] (or null)
+  uint8_t* r_accept;
   // fused SMC iteration: the tile's last workgroup runs temper -> reweight ->
   // next resampling indices (tile.h) on loglik_out right after the sweep
   int has_tail;
@@ -684,6 +686,13 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
 #ifdef SMCDET_TRACE
     tr_acc += accept;
 #endif
+    if constexpr (REPLAY) {  // decision trace (tests only; not in the Philox build)
+      if (lane == 0) {
+        const size_t r = ((size_t)k * a.T + t) * N + n;
+        if (a.r_loga) a.r_loga[r] = fmaf(tau, dll, P.hast);
+        if (a.r_accept) a.r_accept[r] = (uint8_t)(accept && P.hast != -INFINITY);
+      }
+    }
     // An edge hit (log prior -inf) is rejected, and the reference caches the
     // rejected -inf log target as -inf * 0 = NaN (kernel.py:125), so every
     // later proposal of this particle in the sweep is rejected too: the state
@@ -758,10 +767,15 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   // waves add into LDS; the workgroup's last wave adds the total to the tile's
   // counter and takes a ticket; the tile's last workgroup writes the rate and
   // re-zeroes counter and ticket (the workspace is zero on entry and exit).
+  // With the fused tail, the tail workgroup (another CU) reads every wave's
+  // loglik_out / rate_out: each wave releases its own stores at agent scope
+  // before it counts itself done, rather than relying on the last wave's
+  // fence being cumulative over the workgroup-scope ones.
+  if constexpr (TAIL) __threadfence();
   if (lane == 0) {
     const int nw = min(kMhWaves, N - (int)blockIdx.x * kMhWaves);
     if (accept && a.K > 0) atomicAdd(&wg_acc, 1);
-    __threadfence_block();
+    if constexpr (!TAIL) __threadfence_block();
     if (atomicAdd(&wg_done, 1) == nw - 1) {
       int32_t* cnt = a.acc_count + t;
       int32_t* ticket = a.acc_count + a.T + t;
@@ -943,6 +957,8 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
     a.r_uloc = replay->uloc;
     a.r_uflux = replay->uflux;
     a.r_uacc = replay->uacc;
+    a.r_loga = replay->trace_loga;
+    a.r_accept = replay->trace_accept;
   }
   hipStream_t st = (hipStream_t)stream;
   const size_t HWp = (size_t)model->H * model->W + kWave;

@@ -10,7 +10,7 @@ data path.  Collectives:
 
 * end of run: `gather_catalogs` assembles every rank's per-tile posterior
   (counts, locs, fluxes, weights, log Z, ESS, iterations, pruned catalogs) on
-  the destination rank (one all_gather of flat float32 buffers per field;
+  the destination rank (one gather to `dst` per field, in its own dtype;
   ~31 MB for 64 tiles x 4096 particles x 10 sources, well under 1 ms on xGMI);
 * optional lockstep (`lockstep=True`): one 4-byte all_reduce(MAX) per SMC
   iteration, reproducing the reference's rule that finished tiles keep
@@ -28,8 +28,12 @@ from ._rng import rank_seed
 from .sampler import SMCsampler
 
 
+def _initialized():
+    return dist.is_available() and dist.is_initialized()
+
+
 def world():
-    if dist.is_available() and dist.is_initialized():
+    if _initialized():
         return dist.get_rank(), dist.get_world_size()
     return 0, 1
 
@@ -71,16 +75,29 @@ class TileShardedSMC:
             raise ValueError(f"rank {self.rank} has no tiles ({self.num_tiles} tiles, "
                              f"{self.world_size} ranks)")
         seed = rank_seed(seed, self.rank)
+        # pad_mode "partition": each local tile keeps the box of its place in
+        # the whole image's grid (SMCsampler would derive the boxes from the
+        # flat 1 x T_local launch grid otherwise)
+        if "tile_boxes" not in sampler_kwargs and hasattr(Prior, "tile_boxes"):
+            tps = self.tiles_per_side
+            boxes = Prior.tile_boxes((tps, tps))
+            if boxes is not None:
+                sampler_kwargs["tile_boxes"] = boxes[self.start:self.stop]
         self.sampler = SMCsampler.from_tiles(
             local.reshape(1, -1, tile_dim, tile_dim), Prior, ImageModel, MutationKernel,
             num_catalogs, ess_threshold_prop, resample_method, flux_detection_threshold,
             max_smc_iters, print_every, seed=seed, device=device, **sampler_kwargs)
-        if lockstep and self.world_size > 1:
+        # lockstep: the reference's global stop through one 4-byte all_reduce
+        # per SMC iteration (also at world size 1 when a process group exists,
+        # so a single-rank job runs the same collective path)
+        if lockstep and (self.world_size > 1 or _initialized()):
             self.sampler._keep_going = self._keep_going_global
 
     def _keep_going_global(self):
         s = self.sampler
         flag = (s.temperature < 1).any().to(torch.int32).reshape(1)
+        if dist.get_backend(self.group) == "gloo":
+            flag = flag.cpu()  # gloo reduces host tensors; RCCL the device flag
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
         return bool(flag.item())
 
@@ -117,32 +134,32 @@ def gather_tile_results(local: dict, num_tiles: int, tiles_per_side, rank: int,
                         world_size: int, dst: int = 0, group=None):
     """Gathers dicts of [T_local, ...] tensors from every rank into
     [tiles_per_side, tiles_per_side, ...] tensors on `dst` ([num_tiles, ...]
-    when tiles_per_side is None: independent images).  Tensors travel as
-    float32 (integer fields are exact below 2^24) through all_gather on the
-    group's backend (RCCL for GPU tensors, gloo for CPU tensors)."""
+    when tiles_per_side is None: independent images).  One `gather` to `dst`
+    per field, in the field's own dtype (int64 counts stay exact), on the
+    group's backend: RCCL moves device tensors over xGMI, gloo host tensors.
+    Only `dst` receives (and allocates) the assembled catalog."""
     lead = (num_tiles,) if tiles_per_side is None else (tiles_per_side, tiles_per_side)
-    if world_size == 1:
+    if world_size == 1 and not _initialized():
         return {k: v.reshape(*lead, *v.shape[1:]) for k, v in local.items()}
     sizes = [shard_tiles(num_tiles, world_size, r) for r in range(world_size)]
     counts = [b - a for a, b in sizes]
     tmax = max(counts)
     # gloo gathers host tensors: device results are staged through the host
-    # (RCCL gathers device tensors directly, over xGMI)
     host = dist.get_backend(group) == "gloo"
     out = {}
     for k in sorted(local):
         v = local[k]
-        dtype = v.dtype
-        flat = v.reshape(v.shape[0], -1).to(torch.float32)
+        flat = v.reshape(v.shape[0], -1).contiguous()
         if host:
             flat = flat.cpu()
-        pad = torch.zeros(tmax, flat.shape[1], dtype=torch.float32, device=flat.device)
+        # ranks hold T or T+1 tiles (shard_tiles): pad to a common shape
+        pad = torch.zeros(tmax, flat.shape[1], dtype=flat.dtype, device=flat.device)
         pad[: flat.shape[0]] = flat
-        bufs = [torch.empty_like(pad) for _ in range(world_size)]
-        dist.all_gather(bufs, pad, group=group)
+        bufs = [torch.empty_like(pad) for _ in range(world_size)] if rank == dst else None
+        dist.gather(pad, gather_list=bufs, dst=dst, group=group)
         if rank == dst:
             full = torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
-            full = full.reshape(num_tiles, *v.shape[1:]).to(dtype)
+            full = full.reshape(num_tiles, *v.shape[1:]).to(v.device)
             out[k] = full.reshape(*lead, *v.shape[1:])
     return out if rank == dst else None
 

@@ -149,6 +149,16 @@ class SingleComponentMH(object):
             keep = [rc] + ru
             rp = _hip.ReplayC(_hip.ptr(rc).value, _hip.ptr(ru[0]).value, _hip.ptr(ru[1]).value,
                               _hip.ptr(ru[2]).value)
+            # optional decision trace (MH sweep): replay["trace_loga"] float32 /
+            # replay["trace_accept"] uint8 device tensors [K,numH,numW,N]
+            for fld, dt in (("trace_loga", torch.float32), ("trace_accept", torch.uint8)):
+                buf = replay.get(fld)
+                if buf is not None:
+                    if (not buf.is_cuda or buf.dtype != dt or not buf.is_contiguous()
+                            or buf.numel() != self.num_iters * T * N):
+                        raise ValueError(f"replay['{fld}'] must be a contiguous {dt} device "
+                                         f"tensor of {self.num_iters * T * N} elements")
+                    setattr(rp, fld, buf.data_ptr())
         off = self.rng.take(self.num_iters)
         if tail is not None and tail_take:
             tail.offset = self.rng.take(tail_take)

@@ -676,6 +676,14 @@ class SMCsampler(object):
         self.iter = int(st.get("iter", 0))
         self.rng.load_state(st["rng"])
         self.MutationKernel.rng = self.rng
+        if self.fused and self._pending_idx is None and torch.is_tensor(getattr(self, "weights",
+                                                                               None)):
+            # a checkpoint without the pending indices (taken from a fused=False
+            # run, or an older one): the fused schedule gathers the resampled
+            # ancestors inside the next sweep, so draw them now from the
+            # restored weights (resample -> mutate, sampler.py:231-235), at the
+            # random-stream offset the unfused resample() would have taken
+            self._pending_idx = self.resample_index()
         self._live_valid = False
         self._rate_valid = False
         if "rate_image" in st:

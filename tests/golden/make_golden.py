@@ -847,6 +847,194 @@ def gen_smc_steps():
     save("smc_steps.npz", **out)
 
 
+def _bucketize_systematic(W, U):
+    """The reference's systematic indices (sampler.py:136-150) for one tile."""
+    N = W.shape[-1]
+    u = (torch.arange(N) + torch.as_tensor(U).reshape(())) / N
+    return torch.bucketize(u, W.cumsum(-1)).clamp(0, N - 1)
+
+
+def gen_smc_steps_4096(N=4096, K=3, n_steps=10, seed=171):
+    """The tile pass at the headline particle count (VERDICT r2 next #1a):
+    the reference's temper (brentq, sampler.py:99-125), update_weights
+    (:181-196) and systematic resampling (:127-169) on the log-likelihood
+    vectors of a real run -- one 32x32 M71 tile (c2_moderate image), S=10,
+    N=4096, a short MH sweep (K=3) between steps -- recorded at every SMC
+    iteration: temperature in/out, weights, ESS, log Z in/out, the offset U
+    and the indices.  Step 1 starts at temperature 0 (an increment of ~1e-6,
+    at brentq's xtol); extra cases re-temper the last step's log-likelihoods
+    from temperatures 0.999 / 0.9999 / 0.99999 (increment 1 - tau)."""
+    img = c2_moderate_truth_image()
+    prior, model = m71_prior(32, 10, 10, counts_rate=0.003125), m71_model(32)
+    mh = SingleComponentMH(K, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    torch.manual_seed(seed)
+    s = sampler_for(img, 32, prior, model, mh, N)
+    s.initialize()
+    rows = []
+
+    def tile_pass(resample):
+        tau_in, lz_in = s.temperature.clone(), s.log_normalizing_constant.clone()
+        s.temper()
+        s.update_weights()
+        row = dict(loglik=np32(s.loglik)[0, 0], tau_in=np32(tau_in)[0, 0],
+                   tau_out=np32(s.temperature)[0, 0], logZ_in=np32(lz_in)[0, 0],
+                   W=np32(s.weights)[0, 0], ess=np32(s.ess)[0, 0],
+                   logZ=np32(s.log_normalizing_constant)[0, 0],
+                   lw=np32(s.weights_log_unnorm)[0, 0])
+        if resample:
+            W = s.weights.clone()
+            with Recorder() as rec:
+                s.resample()
+            U = rec.draws[0][1]
+            row["U"] = U.reshape(()).astype(np.float32)
+            row["idx"] = _bucketize_systematic(W[0, 0], U).numpy().astype(np.int64)
+        rows.append(row)
+
+    tile_pass(True)
+    for _ in range(n_steps - 1):
+        s.mutate()
+        tile_pass(True)
+        if bool((s.temperature >= 1).all()):
+            break
+    # temperatures close to 1: increment 1 - tau (the f(1 - tau) >= 0 branch)
+    # or a tiny brentq root; same log-likelihoods as the last step
+    for tau in (0.999, 0.9999, 0.99999):
+        s.temperature = torch.full((1, 1), tau)
+        s.log_normalizing_constant = torch.full((1, 1), -4400.0)
+        tile_pass(False)
+    # ... and brentq roots close to 1 - tau: the same log-likelihoods spread
+    # 200x / 5000x wider (an ESS below rho N already at increment 1 - tau)
+    ll0 = s.loglik.clone()
+    orig_ll = s.ImageModel.loglikelihood
+    for tau, scale in ((0.999, 200.0), (0.99, 5000.0)):
+        s.ImageModel.loglikelihood = lambda *a, scale=scale: ll0 * scale
+        s.temperature = torch.full((1, 1), tau)
+        s.log_normalizing_constant = torch.full((1, 1), -4400.0)
+        tile_pass(True)
+    s.ImageModel.loglikelihood = orig_ll
+    out = {}
+    for i, r in enumerate(rows):
+        for k, v in r.items():
+            out[f"c{i:02d}_{k}"] = v
+    out["n_cases"] = np.int64(len(rows))
+    out["rho_N"] = np.float64(s.ess_threshold)
+    save("smc_steps_4096.npz", **out)
+    print("cases", len(rows), "taus", [float(r["tau_out"]) for r in rows])
+
+
+def gen_mh_teacher(N=1024, K=100, steps=(4, 5, 6), seed=181, min_margin=1e-4):
+    """Teacher-forced MH replay at the headline geometry (VERDICT r2 next
+    #1b): one 32x32 M71 tile (c2_moderate image), S=10, N=1024, K=100, the
+    reference's own SMC run.  For each SMC iteration in `steps` (consecutive)
+    it records the state the reference mutates (after its resampling), the
+    temperature, every draw of SingleComponentMH.run (component, the chosen
+    source's location / flux uniforms, the accept uniform), every accept
+    decision (prob <= alpha, kernel.py:115-116) and the returned state; from
+    the second recorded step on also the resampling indices that link it to
+    the previous step's returned state (sampler.py:127-169).  pin[n] = the
+    first iteration whose decision the float64 oracle makes with a margin
+    |log U - min(log alpha, 0)| < min_margin along the reference's
+    trajectory (K when none): decisions before it are pinned exactly."""
+    import contextlib
+    import io
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import smc_oracle as O
+    from tests._params import o_m71_model, o_m71_prior
+    img = c2_moderate_truth_image()
+    prior, model = m71_prior(32, 10, 10, counts_rate=0.003125), m71_model(32)
+    mh = SingleComponentMH(K, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    torch.manual_seed(seed)
+    s = sampler_for(img, 32, prior, model, mh, N, max_iters=10 ** 6)
+    with contextlib.redirect_stdout(io.StringIO()):
+        s.initialize()
+        s.temper()
+        s.update_weights()
+    out = dict(image=np32(s.image), K=np.int64(K), N=np.int64(N), steps=np.array(steps),
+               locs_min=np32(mh.locs_min), locs_max=np32(mh.locs_max),
+               min_margin=np.float64(min_margin))
+    o_prior, o_model = o_m71_prior(32, 10, 10, counts_rate=0.003125), o_m71_model(32)
+    o_mh = O.MHParams(K, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    for it in range(1, steps[-1] + 1):
+        W = s.weights.clone()
+        locs_prev, fluxes_prev = s.locs.clone(), s.fluxes.clone()
+        with Recorder() as rec:
+            s.resample()
+        idx = _bucketize_systematic(W[0, 0], rec.draws[0][1]).numpy().astype(np.int64)
+        if it not in steps:
+            s.mutate()
+            s.temper()
+            s.update_weights()
+            print("iteration", it, "tau", float(s.temperature), flush=True)
+            continue
+        key = f"s{steps.index(it)}_"
+        # the recorded resampling reproduces the reference's gather exactly
+        assert torch.equal(s.locs[0, 0], locs_prev[0, 0][torch.as_tensor(idx)])
+        tau = float(s.temperature)
+        locs0, fluxes0, counts = s.locs.clone(), s.fluxes.clone(), s.counts.clone()
+        accepts = []
+        usample0, le0 = torch.distributions.Uniform.sample, torch.Tensor.__le__
+        state = {"prob": None}
+
+        def usample(self_, *a, **kw):
+            o = usample0(self_, *a, **kw)
+            state["prob"] = o
+            return o
+
+        def le(self_, other):
+            o = le0(self_, other)
+            if self_ is state["prob"]:
+                accepts.append(o.numpy().copy())
+            return o
+
+        with Recorder() as rec:
+            torch.distributions.Uniform.sample = usample
+            torch.Tensor.__le__ = le
+            try:
+                s.mutate()
+            finally:
+                torch.distributions.Uniform.sample = usample0
+                torch.Tensor.__le__ = le0
+        kinds = [k for k, _ in rec.draws]
+        assert kinds == ["mask", "rand", "rand", "rand"] * K, kinds[:8]
+        masks = np.stack([rec.draws[4 * i][1] for i in range(K)])
+        uloc = np.stack([rec.draws[4 * i + 1][1] for i in range(K)])
+        uflux = np.stack([rec.draws[4 * i + 2][1] for i in range(K)])
+        uacc = np.stack([rec.draws[4 * i + 3][1] for i in range(K)]).astype(np.float32)
+        comp = masks.argmax(-1).astype(np.int32)                      # [K,1,1,N]
+        j = comp[..., None]
+        uloc_sel = np.take_along_axis(uloc, j[..., None].repeat(2, -1), axis=-2)[..., 0, :]
+        uflux_sel = np.take_along_axis(uflux, j, axis=-1)[..., 0]
+        accept = np.stack(accepts)
+        assert accept.shape == comp.shape
+        # float64 oracle along the reference's draws: decision margins
+        _, _, _, loga, oacc = O.mh_sweep(np32(s.tiled_image), np32(counts), np32(locs0),
+                                         np32(fluxes0), np.full((1, 1), tau), o_prior, o_model,
+                                         o_mh, comp, uloc_sel, uflux_sel, uacc, trace=True)
+        with np.errstate(all="ignore"):
+            marg = np.abs(np.log(uacc.astype(np.float64)) - np.minimum(loga, 0))
+        marg = np.where(np.isnan(marg), np.inf, marg)[:, 0, 0]          # [K,N]
+        low = marg < min_margin
+        pin = np.where(low.any(0), low.argmax(0), K).astype(np.int16)
+        # where pinned, the oracle decides exactly as the reference did
+        pinned = np.arange(K)[:, None] < pin[None, :]
+        assert np.array_equal(oacc[:, 0, 0][pinned], accept[:, 0, 0][pinned]), \
+            "oracle and reference disagree on a pinned decision"
+        print(f"step {it}: tau {tau:.6f}, pinned decisions {int(pinned.sum())} of {K * N}, "
+              f"particles fully pinned {int((pin == K).sum())}, accept rate "
+              f"{accept.mean():.3f}", flush=True)
+        out.update({key + "tau": np.float32(tau), key + "idx": idx,
+                    key + "counts": np32(counts), key + "locs0": np32(locs0),
+                    key + "fluxes0": np32(fluxes0), key + "comp": comp.astype(np.int8),
+                    key + "uloc": uloc_sel.astype(np.float32),
+                    key + "uflux": uflux_sel.astype(np.float32), key + "uacc": uacc,
+                    key + "accept": accept, key + "locs1": np32(s.locs),
+                    key + "fluxes1": np32(s.fluxes), key + "acc": np32(s.mutation_acc_rates),
+                    key + "pin": pin})
+        s.temper()
+        s.update_weights()
+    save("mh_teacher_c2.npz", **out)
+
+
 def run_smc_recorded(image, tile_dim, prior, model, mh, N, method, seed, max_iters):
     torch.manual_seed(seed)
     s = sampler_for(image, tile_dim, prior, model, mh, N, method=method, max_iters=max_iters)
@@ -957,6 +1145,15 @@ def gen_stats(which, seeds, part=None):
         pr = m71_prior(32, 10, 10, counts_rate=0.003125)
         mk = lambda: SingleComponentMH(20, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])  # noqa
         model, tile, N, method = m71_model(32), 32, 512, "systematic"
+        max_iters = 1000
+    elif which in ("c2_moderate_4096", "c2_moderate_4096_k100"):
+        # the same image at the headline particle count N=4096 (BASELINE
+        # configs[1]); K=20 for >= 20 seeds, K=100 (the headline K) for a few
+        img = c2_moderate_truth_image()
+        pr = m71_prior(32, 10, 10, counts_rate=0.003125)
+        K = 100 if which.endswith("k100") else 20
+        mk = lambda: SingleComponentMH(K, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])  # noqa
+        model, tile, N, method = m71_model(32), 32, 4096, "systematic"
         max_iters = 1000
     elif which == "c2_reduced":
         # the headline geometry (one 32x32 M71 tile, S=10,
@@ -1201,6 +1398,10 @@ if __name__ == "__main__":
         gen_mcmc()
         gen_mcmc_edge()
         gen_agg()
+    elif what == "steps4096":
+        gen_smc_steps_4096()
+    elif what == "mh-teacher":
+        gen_mh_teacher()
     elif what == "mala":
         gen_mala()
     elif what == "mh-edge":

@@ -56,7 +56,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_hip.ImageModelC) == 4 * 4 + 4 * 2 + 6 * 4 + 3 * 4
     assert ctypes.sizeof(_hip.PriorC) == 3 * 4 + 7 * 4
     assert ctypes.sizeof(_hip.MHC) == 4 + 8 * 4
-    assert ctypes.sizeof(_hip.ReplayC) == 4 * ctypes.sizeof(ctypes.c_void_p)
+    assert ctypes.sizeof(_hip.ReplayC) == 6 * ctypes.sizeof(ctypes.c_void_p)
 
 
 def test_invalid_arguments_fail_loudly_without_gpu():

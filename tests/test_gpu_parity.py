@@ -163,6 +163,51 @@ def test_temper_update_weights_vs_reference():
     np.testing.assert_allclose(N(lz), d["weights_logZ"], rtol=1e-6, atol=1e-4)
 
 
+def test_tile_pass_4096_vs_reference():
+    """The tile kernel at the headline N=4096 (8 log-likelihoods per thread of
+    the 512-thread tile kernel) against the reference's temper / update_weights
+    / systematic resampling on a real 32x32 S=10 run's log-likelihoods
+    (make_golden.py gen_smc_steps_4096; 15 cases, run as 15 tiles of one
+    smcdet_temper_reweight launch): increments within 2e-6 of brentq's, W to
+    rtol 1e-5, ESS and log Z; the indices bit-exact from the reference's
+    weights and offset, and from the kernel's own weights up to bins that
+    float32 rounding moves by an ulp."""
+    from smcdet_amd import _hip
+    d = golden("smc_steps_4096.npz")
+    n = int(d["n_cases"])
+    cases = [{k[4:]: d[k] for k in d.files if k.startswith(f"c{i:02d}_")} for i in range(n)]
+    Np = cases[0]["loglik"].size
+    assert Np == 4096
+    ll = T(np.stack([c["loglik"] for c in cases]))
+    tau = T(np.array([float(c["tau_in"]) for c in cases], np.float32))
+    prev = torch.empty_like(tau)
+    lz = T(np.array([float(c["logZ_in"]) for c in cases], np.float32))
+    lw, W = torch.empty_like(ll), torch.empty_like(ll)
+    ess = torch.empty_like(tau)
+    idx = torch.empty(ll.shape, device=DEV, dtype=torch.int64)
+    _hip.check(_hip.lib().smcdet_temper_reweight(
+        _hip.ptr(ll), _hip.ptr(tau), _hip.ptr(prev), _hip.ptr(lw), _hip.ptr(W), _hip.ptr(ess),
+        _hip.ptr(lz), n, Np, float(d["rho_N"]), _hip.SMCDET_RESAMPLE_SYSTEMATIC, 7, 0,
+        _hip.ptr(idx), 0, None, 0, None, None, None, _hip.stream_of(ll)), "temper_reweight")
+    tau_out = np.array([float(c["tau_out"]) for c in cases])
+    tau_in = np.array([float(c["tau_in"]) for c in cases])
+    np.testing.assert_allclose(N(tau) - tau_in, tau_out - tau_in, rtol=0, atol=2e-6)
+    np.testing.assert_array_equal(N(prev), tau_in.astype(np.float32))
+    np.testing.assert_allclose(N(W), np.stack([c["W"] for c in cases]), rtol=1e-5, atol=1e-12)
+    np.testing.assert_allclose(N(ess), [float(c["ess"]) for c in cases], rtol=1e-5)
+    np.testing.assert_allclose(N(lz), [float(c["logZ"]) for c in cases], rtol=1e-6, atol=1e-4)
+    assert N(idx).min() >= 0 and N(idx).max() < Np
+    rs = [i for i, c in enumerate(cases) if "idx" in c]
+    assert len(rs) >= 10
+    Wref = np.stack([cases[i]["W"] for i in rs])[None]
+    U = np.array([[float(cases[i]["U"]) for i in rs]], np.float32)
+    ref_idx = np.stack([cases[i]["idx"] for i in rs])
+    np.testing.assert_array_equal(_resample_idx(Wref, U)[0], ref_idx)
+    own = _resample_idx(N(W)[rs][None], U)[0]
+    diff = own != ref_idx
+    assert diff.sum(-1).max() <= 4, diff.sum(-1)
+
+
 def _resample_idx(W, U):
     from smcdet_amd import _hip
     W = T(W)

@@ -49,9 +49,9 @@ def grid_image(tps, seed=5):
     return img
 
 
-def sampler(image_or_tiles, seed, stopping="independent", tiles=False):
+def sampler(image_or_tiles, seed, stopping="independent", tiles=False, n=N, k=K):
     from smcdet_amd.sampler import SMCsampler
-    args = (p_m71_prior(H, S, S, counts_rate=0.003125), p_m71_model(H), p_m71_mh(K), N, 0.5,
+    args = (p_m71_prior(H, S, S, counts_rate=0.003125), p_m71_model(H), p_m71_mh(k), n, 0.5,
             "systematic", M71["flux_detection_threshold"], 300)
     kw = dict(print_every=10 ** 9, seed=seed, stopping=stopping)
     if tiles:
@@ -126,30 +126,71 @@ def test_world1_gloo_gather_equals_single_process():
     assert int(out["iter"].flatten()[0]) == single.iter
 
 
-def test_two_process_gloo_gather_on_device(tmp_path):
-    """torchrun --nproc-per-node 2 (gloo; both ranks on cuda:0) runs
-    scripts/sharded_check.py: every rank samples its shard, rank 0 gathers
-    and saves the catalogs; they must equal the single-process runs of the
-    two shards' tiles."""
-    from smcdet_amd._rng import rank_seed
+def _torchrun(tmp_path, nproc, **env_extra):
+    """scripts/sharded_check.py under torchrun: every rank samples its shard,
+    rank 0 gathers the catalogs (one gather per field) and saves them."""
     out = tmp_path / "gathered.pt"
-    env = dict(os.environ, SMCDET_SHARD_OUT=str(out), PYTHONPATH=ROOT)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
-           os.path.join(ROOT, "scripts", "sharded_check.py")]
+    env = dict(os.environ, SMCDET_SHARD_OUT=str(out), PYTHONPATH=ROOT,
+               **{k: str(v) for k, v in env_extra.items()})
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.join(ROOT, "scripts", "sharded_check.py")]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    got = torch.load(out, weights_only=True)
-    img = grid_image(2, seed=7)
-    tiles = img.unfold(0, H, H).unfold(1, H, H).reshape(1, 4, H, H)
-    for rank, (a, b) in enumerate(((0, 2), (2, 4))):
-        alone = sampler(tiles[:, a:b].contiguous(), rank_seed(31, rank), tiles=True)
+    return torch.load(out, weights_only=True), r.stdout
+
+
+def _check_gathered(got, img, shards, n=N, k=K, stopping="independent"):
+    """The gathered catalogs equal single-process runs of each rank's tiles
+    (with that rank's seed), field by field and bit for bit, in the
+    single-process dtypes."""
+    from smcdet_amd._rng import rank_seed
+    nt = (img.shape[0] // H) ** 2
+    tiles = img.unfold(0, H, H).unfold(1, H, H).reshape(1, nt, H, H)
+    for rank, (a, b) in enumerate(shards):
+        alone = sampler(tiles[:, a:b].contiguous(), rank_seed(31, rank), tiles=True, n=n, k=k,
+                        stopping=stopping)
         alone.run()
         for f in FIELDS:
             want = flat_tiles(alone, f).cpu()
-            have = got[f].reshape(4, *got[f].shape[2:])[a:b] if got[f].dim() > 2 else \
-                got[f].reshape(4)[a:b]
-            assert torch.equal(have.to(want.dtype), want), (rank, f)
+            have = got[f].reshape(nt, *got[f].shape[2:])[a:b] if got[f].dim() > 2 else \
+                got[f].reshape(nt)[a:b]
+            assert have.dtype == want.dtype, (f, have.dtype, want.dtype)
+            assert torch.equal(have, want), (rank, f)
+
+
+def test_two_process_gloo_gather_on_device(tmp_path):
+    """torchrun --nproc-per-node 2 (gloo; both ranks on cuda:0): the gathered
+    catalogs equal the single-process runs of the two shards' tiles."""
+    got, _ = _torchrun(tmp_path, 2)
+    _check_gathered(got, grid_image(2, seed=7), ((0, 2), (2, 4)))
+
+
+def test_rccl_world1_lockstep_gather(tmp_path):
+    """The RCCL code path on one GPU: a world-size-1
+    "nccl" process group (device_id cuda:0) in a fresh torchrun process runs
+    TileShardedSMC with the reference's lockstep stop (one RCCL all_reduce
+    per SMC iteration) and gathers the catalogs with RCCL gathers of device
+    tensors; they equal the single-process lockstep sampler's attributes."""
+    got, log = _torchrun(tmp_path, 1, SMCDET_SHARD_BACKEND="nccl", SMCDET_SHARD_STOP="lockstep")
+    assert "cuda:0" in log, log
+    img = grid_image(2, seed=7)
+    single = sampler(img, 31, stopping="lockstep")
+    single.run()
+    for f in FIELDS:
+        have, want = got[f], getattr(single, f).cpu()
+        assert have.dtype == want.dtype, (f, have.dtype, want.dtype)
+        assert torch.equal(have, want), f
+    assert int(got["iter"].flatten()[0]) == single.iter
+
+
+def test_c3_two_process_gloo_full_size(tmp_path):
+    """BASELINE configs[2] at full size over two ranks (torchrun, gloo, both
+    on cuda:0): 64 32x32 tiles, N=4096, K=100, 32 tiles per rank; the
+    gathered catalogs equal single-process runs of each rank's 32 tiles."""
+    got, _ = _torchrun(tmp_path, 2, SMCDET_SHARD_TPS=8, SMCDET_SHARD_IMG_SEED=9,
+                       SMCDET_SHARD_N=4096, SMCDET_SHARD_K=100)
+    _check_gathered(got, grid_image(8, seed=9), ((0, 32), (32, 64)), n=4096, k=100)
 
 
 def test_c3_shape_grid_of_32x32_tiles():
@@ -192,3 +233,52 @@ def test_c3_shape_grid_of_32x32_tiles():
     # log Z is fixed once a tile reaches temperature 1 (delta = 0), so the two
     # modes agree on it even though lockstep keeps mutating finished tiles
     assert torch.equal(ind.log_normalizing_constant, s.log_normalizing_constant)
+
+
+def test_c3_full_size_lockstep():
+    """BASELINE configs[2] (C3) at its configured size through one
+    SMCsampler, the reference's tiling (smcdet/sampler.py:28-31) and lockstep
+    stop (:230): an 8x8 grid of 32x32 tiles (a 256x256 image), N=4096, K=100.
+    Every tile reaches temperature 1 with a finite log Z; every non-final step
+    whose increment is >= 1e-3 has ESS = rho*N within 1%; the independent-stop
+    run of the same image and seed finishes every tile at the same iteration
+    with the same log Z; and a sampler over the first two tiles alone
+    reproduces them bit for bit (draws are keyed by tile-local particle)."""
+    Nc, Kc = 4096, 100
+    img = grid_image(8, seed=10)
+    s = sampler(img, 51, stopping="lockstep", n=Nc, k=Kc)
+    esses, taus = [], []
+    orig = s._temper_reweight
+
+    def tr(with_resample, orig=orig):
+        orig(with_resample)
+        esses.append(s.ess.detach().clone())
+        taus.append(s.temperature.detach().clone())
+
+    s._temper_reweight = tr
+    s.run()
+    assert s.locs.shape == (8, 8, Nc, S, 2)
+    assert float(s.temperature.min()) == 1.0
+    assert torch.isfinite(s.log_normalizing_constant).all()
+    assert torch.isfinite(s.ess).all() and float(s.ess.min()) > 0
+    it = s.iters_per_tile.cpu().numpy()
+    assert (it > 0).all() and s.iter == it.max()
+    E = torch.stack(esses).cpu().numpy()
+    Tt = torch.stack(taus).cpu().numpy()
+    checked = 0
+    for t in range(64):
+        h, w = divmod(t, 8)
+        inner = E[: it[h, w], h, w]
+        delta = np.diff(np.concatenate([[0.0], Tt[: it[h, w], h, w]]))
+        np.testing.assert_allclose(inner[delta >= 1e-3], 0.5 * Nc, rtol=0.01)
+        checked += int((delta >= 1e-3).sum())
+    assert checked >= 64 * 5
+    ind = sampler(img, 51, stopping="independent", n=Nc, k=Kc)
+    ind.run()
+    assert torch.equal(ind.iters_per_tile, s.iters_per_tile)
+    assert torch.equal(ind.log_normalizing_constant, s.log_normalizing_constant)
+    tiles = img.unfold(0, H, H).unfold(1, H, H).reshape(1, 64, H, H)[:, :2].contiguous()
+    two = sampler(tiles, 51, stopping="independent", tiles=True, n=Nc, k=Kc)
+    two.run()
+    for f in FIELDS:
+        assert torch.equal(flat_tiles(two, f), flat_tiles(ind, f)[:2]), f

@@ -279,3 +279,56 @@ def test_c_oracle_mh_chain_edge_freeze():
     plan = d["edge_plan"]
     for th, tw, j, k in plan:
         assert d["accept"][th, tw, k:].sum() == 0
+
+
+def _steps4096_cases():
+    d = golden("smc_steps_4096.npz")
+    return d, [{k[4:]: d[k] for k in d.files if k.startswith(f"c{i:02d}_")}
+               for i in range(int(d["n_cases"]))]
+
+
+def test_tile_pass_4096_oracle():
+    """The reference's temper / update_weights / systematic resampling at the
+    headline N=4096 (make_golden.py gen_smc_steps_4096: the log-likelihoods
+    of a real 32x32 S=10 run, temperature 0 -> 0.14, plus temperatures near 1
+    and a root 1e-5 above tau=0.99): the oracle's Brent reproduces brentq's
+    increments, its weights / ESS / log Z and its indices the reference's."""
+    d, cases = _steps4096_cases()
+    assert len(cases) >= 12
+    for c in cases:
+        ll = c["loglik"].reshape(1, 1, -1)
+        tau_in = c["tau_in"].reshape(1, 1)
+        tau, _ = O.temper(ll, tau_in, float(d["rho_N"]))
+        np.testing.assert_allclose(tau.ravel(), c["tau_out"].ravel(), rtol=0, atol=2e-6)
+        W, ess, lz = O.update_weights(ll, c["tau_out"].reshape(1, 1), tau_in,
+                                      c["logZ_in"].reshape(1, 1), ll.shape[-1])
+        np.testing.assert_allclose(W.ravel(), c["W"], rtol=1e-5, atol=1e-12)
+        np.testing.assert_allclose(float(ess.ravel()[0]), float(c["ess"]), rtol=1e-5)
+        np.testing.assert_allclose(float(lz.ravel()[0]), float(c["logZ"]), rtol=1e-6, atol=1e-4)
+        if "idx" in c:
+            idx = O.systematic_resample_index(c["W"].reshape(1, 1, -1), c["U"].reshape(1, 1))
+            np.testing.assert_array_equal(idx.ravel(), c["idx"])
+
+
+def test_c_oracle_teacher_forced_c2():
+    """The C restatement replays the reference's recorded headline-geometry
+    sweeps (make_golden.py gen_mh_teacher: 32x32, S=10, N=1024, K=100, three
+    SMC iterations): every particle whose decisions the float64 oracle makes
+    with margins >= 1e-4 ends in the reference's state."""
+    from oracle import c_oracle
+    d = golden("mh_teacher_c2.npz")
+    K = int(d["K"])
+    prior, model = o_m71_prior(32, 10, 10, counts_rate=0.003125), o_m71_model(32)
+    mh = o_m71_mh(K)
+    img = d["image"].reshape(1, 1, 32, 32)
+    for i in range(len(d["steps"])):
+        k = f"s{i}_"
+        replay = {"comp": d[k + "comp"].astype(np.int32), "uloc": d[k + "uloc"],
+                  "uflux": d[k + "uflux"], "uacc": d[k + "uacc"]}
+        l1, f1, _ = c_oracle.mh_sweep(img, d[k + "counts"], d[k + "locs0"], d[k + "fluxes0"],
+                                      float(d[k + "tau"]), prior, model, mh, replay=replay)
+        full = d[k + "pin"] == K
+        assert full.mean() > 0.98
+        np.testing.assert_allclose(l1[0, 0][full], d[k + "locs1"][0, 0][full], rtol=0, atol=2e-5)
+        np.testing.assert_allclose(f1[0, 0][full], d[k + "fluxes1"][0, 0][full], rtol=2e-6,
+                                   atol=1e-3)
