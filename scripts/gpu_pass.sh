@@ -9,7 +9,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-STEPS=${STEPS:-"pytest smoke bench torchrun1 profile"}
+STEPS=${STEPS:-"pytest smoke bench torchrun1 profile large"}
 step() {
   echo "$1 rc=$2"
   if [ "$2" -ne 0 ] && [ "$2" -ne 1 ]; then echo "stopping after $1"; exit "$2"; fi
@@ -17,7 +17,8 @@ step() {
 has() { [[ " $STEPS " == *" $1 "* ]]; }
 if has pytest; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 \
-    --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+    --timeout-method thread ${PYTEST_ARGS:---ignore=tests/test_gpu_large_tile.py} \
+    > gpurun_out/pytest_gpu.log 2>&1
   step pytest $?
   grep -E "^FAILED|passed|failed" gpurun_out/pytest_gpu.log | tail -8
 fi
@@ -43,4 +44,10 @@ if has profile; then
     bash scripts/profile.sh
   step profile $?
   cat gpurun_out/prof/summary.txt | tail -20
+fi
+if has large; then  # the global-memory (large-tile) paths, last
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_large_tile.py -v -p no:cacheprovider \
+    --timeout 200 --timeout-method thread > gpurun_out/pytest_large.log 2>&1
+  step large $?
+  grep -E "^FAILED|passed|failed" gpurun_out/pytest_large.log | tail -8
 fi

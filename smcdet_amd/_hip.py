@@ -30,6 +30,9 @@ SMCDET_SMC_TWO_LAUNCH = 2
 # Shapes the kernels support (checked by the C ABI too; the samplers raise
 # ValueError at construction with these named, SMCsampler/MHsampler.__init__):
 MAX_TILE_PIXELS = 4096      # H*W: the tile image + one rate image per wave in LDS (64x64)
+# SingleComponentMH SMC with the M71 model above MAX_TILE_PIXELS: the global-memory
+# sweep (tile image L2-resident, rate images in HBM), up to 256x256
+MAX_TILE_PIXELS_GLOBAL = 65536
 MAX_SOURCES = 64            # S = Prior.max_objects: one source per lane
 MAX_PARTICLES = 16384       # N per tile: the tile kernel holds 32 log-likelihoods per thread
 MAX_TILES = 65535           # T: the MH grid's y dimension
@@ -37,13 +40,20 @@ MAX_PSF_RADIUS = 64
 MAX_AGG_SOURCES = 256       # sources of an aggregated (joint) tile: catalog in LDS
 
 
-def check_limits(H, W, S, N=None, T=None, R=None, where="sampler"):
+def check_limits(H, W, S, N=None, T=None, R=None, where="sampler", global_ok=False):
     """ValueError naming the limit a configuration exceeds (the reference has
-    none: smcdet/sampler.py:25-31 tiles any image)."""
-    if H * W > MAX_TILE_PIXELS:
-        raise ValueError(f"{where}: a {H}x{W} tile has {H * W} pixels; the gfx950 kernels keep "
-                         f"the tile and one rate image per wavefront in LDS, at most "
-                         f"{MAX_TILE_PIXELS} pixels (64x64) -- use tile_dim <= 64")
+    none: smcdet/sampler.py:25-31 tiles any image).  global_ok: the caller
+    runs the global-memory paths above MAX_TILE_PIXELS (SingleComponentMH with
+    the M71 image model, up to MAX_TILE_PIXELS_GLOBAL)."""
+    if global_ok and H * W > MAX_TILE_PIXELS:
+        if H * W > MAX_TILE_PIXELS_GLOBAL:
+            raise ValueError(f"{where}: a {H}x{W} tile has {H * W} pixels, above the "
+                             f"{MAX_TILE_PIXELS_GLOBAL} (256x256) of the global-memory sweep")
+    elif H * W > MAX_TILE_PIXELS:
+        raise ValueError(f"{where}: a {H}x{W} tile has {H * W} pixels; this path keeps the "
+                         f"tile and one rate image per wavefront in LDS, at most "
+                         f"{MAX_TILE_PIXELS} pixels (64x64) -- use tile_dim <= 64 (SMC with "
+                         f"SingleComponentMH and M71ImageModel runs tiles up to 256x256)")
     if S > MAX_SOURCES:
         raise ValueError(f"{where}: max_objects = {S} > {MAX_SOURCES} (one source per lane of a "
                          "64-wide wavefront)")

@@ -54,12 +54,17 @@ static void timing_free() {
   g_tcap = g_tused = 0;
 }
 
-int validate_model(const smcdet_image_model_t* m) {
+int validate_model(const smcdet_image_model_t* m, int max_pixels) {
   if (!m) return set_error(SMCDET_EINVAL, "image model is null");
   if (m->model != SMCDET_MODEL_M71 && m->model != SMCDET_MODEL_POISSON)
     return set_error(SMCDET_EINVAL, "unknown image model %d", m->model);
-  if (m->H <= 0 || m->W <= 0 || m->H * m->W > 4096)
-    return set_error(SMCDET_EUNSUPPORTED, "tile %dx%d outside 1..4096 pixels", m->H, m->W);
+  if (m->H <= 0 || m->W <= 0 || (int64_t)m->H * m->W > max_pixels)
+    return set_error(SMCDET_EUNSUPPORTED, "tile %dx%d outside 1..%d pixels", m->H, m->W,
+                     max_pixels);
+  if (m->model == SMCDET_MODEL_POISSON && m->H * m->W > kMaxLdsPixels)
+    return set_error(SMCDET_EUNSUPPORTED,
+                     "tile %dx%d: tiles above %d pixels run the M71 image model only", m->H,
+                     m->W, kMaxLdsPixels);
   if (m->psf_radius < 0 || m->psf_radius > 64)
     return set_error(SMCDET_EUNSUPPORTED, "psf_radius %d outside 0..64", m->psf_radius);
   return SMCDET_OK;

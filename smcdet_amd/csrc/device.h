@@ -281,7 +281,12 @@ struct DevModel {
 };
 
 DevModel make_dev_model(const smcdet_image_model_t& m);  // common.hip
-int validate_model(const smcdet_image_model_t* m);        // common.hip
+// tiles whose image and per-wave rate images fit LDS; larger tiles (up to
+// kMaxGlobalPixels) run the global-memory paths (M71 model: smcdet_loglik,
+// smcdet_render, smcdet_mh_sweep)
+constexpr int kMaxLdsPixels = 4096;
+constexpr int kMaxGlobalPixels = 65536;
+int validate_model(const smcdet_image_model_t* m, int max_pixels = kMaxLdsPixels);  // common.hip
 
 // M71ImageModel._compute_normalized_psf (images.py:137-145) / the basic
 // model's Normal(0, sigma).log_prob(r).exp() (images.py:17, 25-26)

@@ -149,7 +149,9 @@ __device__ __forceinline__ void propose_lane(float mu, float c_ph, float c_lZ, f
 // One position of the union window: rate change dl and log-likelihood change.
 // WINDOWS = false when old and new windows coincide (same floor anchors): every
 // position of the (clipped) box is in both.
-template <int MODEL, bool WINDOWS>
+// GL: the tile image lives in global memory (tiles above the LDS budget): a
+// masked lane's dummy position HW + lane reads the last pixel instead
+template <int MODEL, bool WINDOWS, bool GL = false>
 __device__ __forceinline__ float position_delta(const DevModel& m, const float* xs,
                                                 const float* lg, const float* lam, int p,
                                                 int aa, int bb, int ph, int pw,
@@ -170,14 +172,15 @@ __device__ __forceinline__ float position_delta(const DevModel& m, const float* 
   const float lo = lam[p];
   lnew = lo + dl;
   const float lgx = (MODEL == SMCDET_MODEL_POISSON) ? lg[p] : 0.0f;
-  return pix_delta<MODEL>(m, xs[p], lgx, lo, dl);
+  const float x = GL ? xs[min(p, m.H * m.W - 1)] : xs[p];
+  return pix_delta<MODEL>(m, x, lgx, lo, dl);
 }
 
 // Two positions per lane at once (union-window slots 2i and 2i+1): the float
 // arithmetic runs as packed v_pk_{fma,mul,add}_f32 (one issue for both
 // halves), the transcendentals per half.  Same per-element operation order as
 // position_delta.
-template <int MODEL, bool WINDOWS>
+template <int MODEL, bool WINDOWS, bool GL = false>
 __device__ __forceinline__ f2 position_delta2(const DevModel& m, const float* xs, const float* lg,
                                              const float* lam, const int (&p)[2],
                                              const int (&aa)[2], const int (&bb)[2], f2 fph,
@@ -199,7 +202,13 @@ __device__ __forceinline__ f2 position_delta2(const DevModel& m, const float* xs
   }
   const f2 dl = fma2(psi_n, amp_n, -amp_o * psi_o);
   const f2 lo = {lam[p[0]], lam[p[1]]};
-  const f2 x = {xs[p[0]], xs[p[1]]};
+  f2 x;
+  if constexpr (GL) {
+    const int hw1 = m.H * m.W - 1;
+    x = f2{xs[min(p[0], hw1)], xs[min(p[1], hw1)]};
+  } else {
+    x = f2{xs[p[0]], xs[p[1]]};
+  }
   lnew = lo + dl;
   f2 lgx = {0.f, 0.f};
   if constexpr (MODEL == SMCDET_MODEL_POISSON) lgx = f2{lg[p[0]], lg[p[1]]};
@@ -228,7 +237,11 @@ constexpr int mh_slots() { return PPL == 1 ? 1 : kSlots; }
 // TAIL: the fused SMC step's instantiation (a.has_tail); the sweep alone
 // compiles without the tail pass, which would otherwise raise its SGPR
 // pressure (spills reloaded by v_readlane in the loop).
-template <int MODEL, bool REPLAY, bool FULL, int PPL, bool PAIRED, bool TAIL>
+// GL: tiles above the LDS budget (M71, PPL = 0): the tile image is read from
+// global memory (L2-resident) and the particle's rate image lives in rate_out
+// (row stride H*W + 64: the 64 dummy cells of masked lanes), which the sweep
+// updates in place; LDS holds only the workgroup counters.
+template <int MODEL, bool REPLAY, bool FULL, int PPL, bool PAIRED, bool TAIL, bool GL = false>
 __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_kernel(MhArgs a) {
   constexpr int NSL = mh_slots<PPL>();
   extern __shared__ float smem[];
@@ -247,14 +260,18 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   float* xs = smem;
   float* lg = smem + HWp;
   float* lam = smem + kImg * HWp + wave * HWp;
-
-  stage_image<MODEL>(a.img + (size_t)t * HW, xs, lg, HW, threadIdx.x, kMhBlock);
+  if constexpr (GL) {
+    xs = const_cast<float*>(a.img) + (size_t)t * HW;
+    lg = nullptr;
+  } else {
+    stage_image<MODEL>(a.img + (size_t)t * HW, xs, lg, HW, threadIdx.x, kMhBlock);
+  }
   if (threadIdx.x == 0) {
     wg_acc = 0;
     wg_done = 0;
     wg_last = 0;
   }
-  if (threadIdx.x < kWave) {
+  if (!GL && threadIdx.x < kWave) {
     xs[HW + threadIdx.x] = m.bg;
     if (MODEL == SMCDET_MODEL_POISSON) lg[HW + threadIdx.x] = 0.f;
   }
@@ -266,6 +283,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   const int N = a.N, S = a.S;
   const size_t pid = (size_t)t * N + n;
   const size_t src = a.ancestors ? (size_t)t * N + (size_t)a.ancestors[pid] : pid;
+  if constexpr (GL) lam = a.rate_out + pid * (size_t)HWp;
   const float count = a.counts_in[src];
   if (a.counts_out && lane == 0) a.counts_out[pid] = count;
   // range of the moved component: 0..S-1 (kernel.py:35-37), or 0..count-1
@@ -286,7 +304,19 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   SMC_TRACE(trow, 2);
 
   double cur_ll = 0.0;  // tracked only in FULL mode (incremental mode works on deltas)
-  if constexpr (!FULL) {
+  if constexpr (GL && !FULL) {
+    // the working image is rate_out's row: copy the ancestor's row in, or render
+    if (a.rate_in && !(a.rate_in == a.rate_out && src == pid)) {
+      const float* rin = a.rate_in + src * (size_t)HWp;
+      for (int p = lane; p < HW; p += kWave) lam[p] = rin[p];
+      wave_sync();
+    } else if (!a.rate_in) {
+      render_chunks<MODEL>(m, lam, sh, sw, sfx, S, lane);
+    }
+  } else if constexpr (GL) {
+    render_sources<MODEL>(m, lam, sh, sw, sfx, S, lane);
+    cur_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
+  } else if constexpr (!FULL) {
     if (a.rate_in) {
       // the ancestor's rate image, persisted by the previous sweep: no render
       const float* rin = a.rate_in + src * (size_t)HW;
@@ -530,7 +560,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           const int ph = r0 + aa, pw = c0 + bb;
           const int p = valid ? (int)__umul24((unsigned)ph, (unsigned)m.W) + pw : HW + lane;
           float lnew;
-          const float e = position_delta<MODEL, win>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
+          const float e = position_delta<MODEL, win, GL>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
                                                      amp_n, ao_h, ao_w, an_h, an_w, lnew);
           acc += valid ? e : 0.f;
           s_lam[i] = lnew;
@@ -562,7 +592,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
             fpw[h] = (float)pw + 0.5f;
           }
           f2 lnew;
-          f2 e = position_delta2<MODEL, win>(m, xs, lg, lam, p, aa, bb, fph, fpw, P, amp_o, amp_n,
+          f2 e = position_delta2<MODEL, win, GL>(m, xs, lg, lam, p, aa, bb, fph, fpw, P, amp_o, amp_n,
                                              ao_h, ao_w, an_h, an_w, lnew);
           e.x = valid[0] ? e.x : 0.f;
           e.y = valid[1] ? e.y : 0.f;
@@ -581,7 +611,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           const int ph = r0 + aa, pw = c0 + bb;
           const int p = valid ? (int)__umul24((unsigned)ph, (unsigned)m.W) + pw : HW + lane;
           float lnew;
-          const float e = position_delta<MODEL, win>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
+          const float e = position_delta<MODEL, win, GL>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
                                                      amp_n, ao_h, ao_w, an_h, an_w, lnew);
           acc1 = valid ? e : 0.f;
           s_lam[2 * np] = lnew;
@@ -612,7 +642,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           const int ph = r0 + aa, pw = c0 + bb;
           const int p = (int)__umul24((unsigned)ph, (unsigned)m.W) + pw;
           float lnew;
-          acc += position_delta<MODEL, true>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o, amp_n,
+          acc += position_delta<MODEL, true, GL>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o, amp_n,
                                              ao_h, ao_w, an_h, an_w, lnew);
           if constexpr (decltype(WRITE)::value) lam[p] = lnew;
         }
@@ -749,7 +779,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     }
     if (lane == 0) a.loglik_out[pid] = (float)ll;
   }
-  if constexpr (!FULL) {
+  if constexpr (!FULL && !GL) {  // (GL: the sweep worked in rate_out's row)
     if (a.rate_out) {
       float* rout = a.rate_out + pid * (size_t)HW;
       if ((HW & 3) == 0) {
@@ -840,9 +870,25 @@ static int launch_mh1(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
   return SMCDET_OK;
 }
 
+// tiles above the LDS budget (M71 only; host-checked): paired slots, no
+// fused tail, no dynamic LDS
+template <int MODEL, bool REPLAY, bool FULL>
+static int launch_mh_gl(const MhArgs& a, dim3 grid, hipStream_t st) {
+  if (a.has_tail || a.scalar_slots)
+    return set_error(SMCDET_EUNSUPPORTED, "tiles above %d pixels: no fused step / scalar slots",
+                     kMaxLdsPixels);
+  constexpr bool kPair = !FULL;
+  launch_sweep(mh_sweep_kernel<MODEL, REPLAY, FULL, 0, kPair, false, true>, grid, dim3(kMhBlock),
+               0, st, a);
+  return SMCDET_OK;
+}
+
 template <int MODEL, bool REPLAY, bool FULL>
 static int launch_mh_ppl(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
   const int HW = a.m.H * a.m.W;
+  if constexpr (MODEL == SMCDET_MODEL_M71) {
+    if (HW > kMaxLdsPixels) return launch_mh_gl<MODEL, REPLAY, FULL>(a, grid, st);
+  }
   if (a.S <= kWave) {
     if (HW <= 64) return launch_mh1<MODEL, REPLAY, FULL, 1>(a, grid, lds, st);
     if (HW <= 256) return launch_mh1<MODEL, REPLAY, FULL, 4>(a, grid, lds, st);
@@ -877,6 +923,7 @@ static bool tail_fusable(const smcdet_image_model_t& m, int N, int S, uint32_t f
   const size_t need = mh_lds > tile_lds_bytes(N) ? mh_lds : tile_lds_bytes(N);
   if (lds) *lds = need;
   if (flags & (SMCDET_MH_FULL_RECOMPUTE | SMCDET_MH_SCALAR_SLOTS)) return false;
+  if (m.H * m.W > kMaxLdsPixels) return false;  // global-memory tiles: two launches
   if (N % kMhWaves != 0 || N > kTailMaxN) return false;
   if (S <= kWave && m.H * m.W <= 64) return false;  // small-tile instantiation (PPL = 1)
   // 4 waves per SIMD = 4 workgroups per CU must still fit the 160 KiB LDS
@@ -895,11 +942,16 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
                          const int32_t* go, const float* tile_boxes,
                          const smcdet_smc_tail_t* tail, void* stream) {
 
-  int rc = validate_model(model);
+  int rc = validate_model(model, kMaxGlobalPixels);
   if (rc) return rc;
   rc = validate_prior(prior);
   if (rc) return rc;
   if (!mh) return set_error(SMCDET_EINVAL, "mh params are null");
+  const bool global_tile = model->H * model->W > kMaxLdsPixels;
+  if (global_tile && !rate_out)
+    return set_error(SMCDET_EINVAL,
+                     "tiles above %d pixels need rate_out [T,N,H*W+64] (the sweep's working "
+                     "rate images)", kMaxLdsPixels);
   if (!tiled_image || !temperature || !counts_in || !locs_in || !fluxes_in || !locs_out ||
       !fluxes_out || !acc_rate || !acc_count)
     return set_error(SMCDET_EINVAL, "null buffer");
@@ -962,7 +1014,7 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
   }
   hipStream_t st = (hipStream_t)stream;
   const size_t HWp = (size_t)model->H * model->W + kWave;
-  size_t lds =
+  size_t lds = global_tile ? 0 :
       ((model->model == SMCDET_MODEL_POISSON ? 2 : 1) * HWp + (size_t)kMhWaves * HWp) *
       sizeof(float);
   const dim3 grid((N + kMhWaves - 1) / kMhWaves, T);

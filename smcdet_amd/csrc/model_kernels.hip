@@ -54,6 +54,58 @@ __global__ __launch_bounds__(kBlock) void loglik_kernel(DevModel m, const float*
   if (lane == 0) out[pid] = (float)ll;
 }
 
+// tiles above the LDS budget (M71): the tile image stays in global memory
+// (L2-resident), the rate image is rendered chunk by chunk in registers
+template <int MODEL>
+__global__ __launch_bounds__(kBlock) void loglik_global_kernel(DevModel m,
+                                                               const float* __restrict__ img,
+                                                               const float* __restrict__ locs,
+                                                               const float* __restrict__ fluxes,
+                                                               int N, int S,
+                                                               float* __restrict__ out) {
+  const int HW = m.H * m.W;
+  const int t = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = blockIdx.x * kWavesPerBlock + wave;
+  if (n >= N) return;
+  const size_t pid = (size_t)t * N + n;
+  float sh = 0.f, sw = 0.f, sf = 0.f;
+  if (lane < S) {
+    sh = locs[(pid * S + lane) * 2 + 0];
+    sw = locs[(pid * S + lane) * 2 + 1];
+    sf = fluxes[pid * S + lane];
+  }
+  const double ll = loglik_chunks<MODEL>(m, img + (size_t)t * HW, sh, sw, sf, S, lane);
+  if (lane == 0) out[pid] = (float)ll;
+}
+
+template <int MODEL>
+__global__ __launch_bounds__(kBlock) void render_global_kernel(DevModel m,
+                                                               const float* __restrict__ locs,
+                                                               const float* __restrict__ fluxes,
+                                                               int N, int S,
+                                                               float* __restrict__ rate) {
+  const int HW = m.H * m.W;
+  const int t = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = blockIdx.x * kWavesPerBlock + wave;
+  if (n >= N) return;
+  const size_t pid = (size_t)t * N + n;
+  float sh = 0.f, sw = 0.f, sf = 0.f;
+  if (lane < S) {
+    sh = locs[(pid * S + lane) * 2 + 0];
+    sw = locs[(pid * S + lane) * 2 + 1];
+    sf = fluxes[pid * S + lane];
+  }
+  const ChunkSrc c = chunk_sources<MODEL>(m, sh, sw, sf, S, lane);
+  const float inv_w = 1.0f / (float)m.W;
+  for (int k = 0; k * kWave < HW; ++k) {
+    const int p = k * kWave + lane;
+    const float v = chunk_rate<MODEL>(m, c, S, k, lane, inv_w);
+    if (p < HW) rate[((size_t)t * HW + p) * N + n] = v;
+  }
+}
+
 // rate[T,H,W,N]
 template <int MODEL>
 __global__ __launch_bounds__(kBlock) void render_kernel(DevModel m, const float* __restrict__ locs,
@@ -253,7 +305,7 @@ extern "C" {
 int smcdet_loglik(const smcdet_image_model_t* model, const float* tiled_image, const float* locs,
                   const float* fluxes, int32_t T, int32_t N, int32_t S, float* out,
                   void* stream) {
-  int rc = validate_model(model);
+  int rc = validate_model(model, kMaxGlobalPixels);
   if (rc) return rc;
   if (!tiled_image || !locs || !fluxes || !out) return set_error(SMCDET_EINVAL, "null buffer");
   if (T <= 0 || N <= 0 || S < 0)
@@ -261,6 +313,13 @@ int smcdet_loglik(const smcdet_image_model_t* model, const float* tiled_image, c
   if (T > 65535) return set_error(SMCDET_EUNSUPPORTED, "T=%d > 65535", T);
   const DevModel m = make_dev_model(*model);
   const dim3 grid((N + kWavesPerBlock - 1) / kWavesPerBlock, T);
+  if (m.H * m.W > kMaxLdsPixels) {  // M71 (validate_model), global-memory path
+    if (S > kWave) return set_error(SMCDET_EUNSUPPORTED, "S=%d > 64 above %d pixels", S,
+                                    kMaxLdsPixels);
+    hipLaunchKernelGGL(loglik_global_kernel<SMCDET_MODEL_M71>, grid, dim3(kBlock), 0,
+                       (hipStream_t)stream, m, tiled_image, locs, fluxes, N, S, out);
+    return check_launch("smcdet_loglik");
+  }
   const size_t lds = model_lds_bytes(*model, 1);
   hipStream_t st = (hipStream_t)stream;
   const int HW = m.H * m.W;
@@ -289,13 +348,20 @@ int smcdet_loglik(const smcdet_image_model_t* model, const float* tiled_image, c
 
 int smcdet_render(const smcdet_image_model_t* model, const float* locs, const float* fluxes,
                   int32_t T, int32_t N, int32_t S, float* rate, void* stream) {
-  int rc = validate_model(model);
+  int rc = validate_model(model, kMaxGlobalPixels);
   if (rc) return rc;
   if (!locs || !fluxes || !rate) return set_error(SMCDET_EINVAL, "null buffer");
   if (T <= 0 || N <= 0 || S < 0 || T > 65535)
     return set_error(SMCDET_EUNSUPPORTED, "T=%d N=%d S=%d", T, N, S);
   const DevModel m = make_dev_model(*model);
   const dim3 grid((N + kWavesPerBlock - 1) / kWavesPerBlock, T);
+  if (m.H * m.W > kMaxLdsPixels) {
+    if (S > kWave) return set_error(SMCDET_EUNSUPPORTED, "S=%d > 64 above %d pixels", S,
+                                    kMaxLdsPixels);
+    hipLaunchKernelGGL(render_global_kernel<SMCDET_MODEL_M71>, grid, dim3(kBlock), 0,
+                       (hipStream_t)stream, m, locs, fluxes, N, S, rate);
+    return check_launch("smcdet_render");
+  }
   const size_t lds = (size_t)kWavesPerBlock * m.H * m.W * sizeof(float);
   hipStream_t st = (hipStream_t)stream;
   rc = ensure_lds(m.model == SMCDET_MODEL_M71 ? (const void*)render_kernel<SMCDET_MODEL_M71>
@@ -313,7 +379,7 @@ int smcdet_render(const smcdet_image_model_t* model, const float* locs, const fl
 
 int smcdet_psf_dense(const smcdet_image_model_t* model, const float* locs, int32_t T, int32_t N,
                      int32_t S, float* psf, void* stream) {
-  int rc = validate_model(model);
+  int rc = validate_model(model, kMaxGlobalPixels);
   if (rc) return rc;
   if (!locs || !psf) return set_error(SMCDET_EINVAL, "null buffer");
   if (T <= 0 || N <= 0 || S <= 0) return set_error(SMCDET_EUNSUPPORTED, "empty shape");
@@ -335,7 +401,7 @@ int smcdet_psf_dense(const smcdet_image_model_t* model, const float* locs, int32
 
 int smcdet_sample_image(const smcdet_image_model_t* model, const float* rate, int64_t count,
                         uint64_t seed, uint64_t offset, float* image, void* stream) {
-  int rc = validate_model(model);
+  int rc = validate_model(model, kMaxGlobalPixels);
   if (rc) return rc;
   if (!rate || !image || count < 0) return set_error(SMCDET_EINVAL, "bad buffer/count");
   if (count == 0) return SMCDET_OK;

@@ -112,6 +112,88 @@ __device__ __forceinline__ void render_regs(const DevModel& m, float (&lamk)[PPL
   }
 }
 
+// ---------------------------------------------------------------------------
+// Tiles of any size (above the LDS budget): pixel-centric chunks of 64
+// pixels, p = 64k + lane.  Lane s precomputes source s's amplitude and the
+// chunk range [klo, khi] its clipped window's rows cover (wave-uniform
+// skips); per pixel the sum order is background, then sources 0..S-1, with
+// render_regs's arithmetic, so a chunk equals render_regs's register for the
+// same pixel.
+// ---------------------------------------------------------------------------
+struct ChunkSrc {
+  float h, w, amp;  // lane s: source s (amp = g * psf_scale * f)
+  int klo, khi;     // chunks its window rows touch (klo > khi: none)
+};
+
+template <int MODEL>
+__device__ __forceinline__ ChunkSrc chunk_sources(const DevModel& m, float sh, float sw, float sf,
+                                                  int S, int lane) {
+  ChunkSrc c;
+  c.h = sh;
+  c.w = sw;
+  c.amp = m.g * psf_scale<MODEL>(m) * sf;
+  const int fh = ifloor_clamped(sh), fw = ifloor_clamped(sw);
+  const int r0 = max(fh - m.R, 0), r1 = min(fh + m.R, m.H - 1);
+  const bool empty = lane >= S || r0 > r1 || fw + m.R < 0 || fw - m.R > m.W - 1;
+  c.klo = empty ? 1 : (r0 * m.W) >> 6;
+  c.khi = empty ? 0 : ((r1 + 1) * m.W - 1) >> 6;
+  return c;
+}
+
+// rate at pixel p = 64k + lane (meaningful for p < H*W)
+template <int MODEL>
+__device__ __forceinline__ float chunk_rate(const DevModel& m, const ChunkSrc& c, int S, int k,
+                                            int lane, float inv_w) {
+  const int p = k * kWave + lane;
+  const int ph = (int)(((float)p + 0.5f) * inv_w);  // exact: p < 2^16, W <= 2^16
+  const int pw = p - ph * m.W;
+  float lam = m.bg;
+  for (int s = 0; s < S; ++s) {
+    if (k < readlane(c.klo, s) || k > readlane(c.khi, s)) continue;
+    const float h = readlane(c.h, s), w = readlane(c.w, s);
+    const float amp = readlane(c.amp, s);
+    const int fh = ifloor_clamped(h), fw = ifloor_clamped(w);
+    const float dh = ((float)ph + 0.5f) - h;
+    const float dw = ((float)pw + 0.5f) - w;
+    const float v = amp * psf_raw<MODEL>(m, fmaf(dh, dh, dw * dw));
+    const bool in = (unsigned)(ph - fh + m.R) <= 2u * (unsigned)m.R &&
+                    (unsigned)(pw - fw + m.R) <= 2u * (unsigned)m.R;
+    lam += in ? v : 0.0f;
+  }
+  return lam;
+}
+
+// full render into a rate image in global memory (lam[p], p < H*W)
+template <int MODEL>
+__device__ __forceinline__ void render_chunks(const DevModel& m, float* lam, float sh, float sw,
+                                              float sf, int S, int lane) {
+  const int HW = m.H * m.W;
+  const float inv_w = 1.0f / (float)m.W;
+  const ChunkSrc c = chunk_sources<MODEL>(m, sh, sw, sf, S, lane);
+  for (int k = 0; k * kWave < HW; ++k) {
+    const float v = chunk_rate<MODEL>(m, c, S, k, lane, inv_w);
+    if (k * kWave + lane < HW) lam[k * kWave + lane] = v;
+  }
+  wave_sync();
+}
+
+// sum of the per-pixel log-likelihood without storing the rate image
+template <int MODEL>
+__device__ __forceinline__ double loglik_chunks(const DevModel& m, const float* __restrict__ x,
+                                                float sh, float sw, float sf, int S, int lane) {
+  const int HW = m.H * m.W;
+  const float inv_w = 1.0f / (float)m.W;
+  const ChunkSrc c = chunk_sources<MODEL>(m, sh, sw, sf, S, lane);
+  float acc = 0.0f;
+  for (int k = 0; k * kWave < HW; ++k) {
+    const int p = k * kWave + lane;
+    const float lam = chunk_rate<MODEL>(m, c, S, k, lane, inv_w);
+    const float e = pix_loglik<MODEL>(m, x[p < HW ? p : HW - 1], 0.0f, lam);
+    acc += p < HW ? e : 0.0f;
+  }
+  return wave_sum((double)acc);
+}
+
 template <int MODEL, int PPL>
 __device__ __forceinline__ double pixel_sum_regs(const DevModel& m, const float* xs,
                                                  const float* lg, const float (&lamk)[PPL],

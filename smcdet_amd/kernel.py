@@ -86,11 +86,19 @@ class SingleComponentMH(object):
         return ws
 
     @staticmethod
-    def _rate_buffer(buf, name, TN, data):
+    def rate_row(H, W):
+        """Row length of a persisted rate image: H*W, or H*W + 64 for tiles
+        above the LDS budget, whose sweep works in the row in global memory
+        (64 dummy cells for masked lanes, smcdet_hip.h)."""
+        return H * W + (64 if H * W > _hip.MAX_TILE_PIXELS else 0)
+
+    @classmethod
+    def _rate_buffer(cls, buf, name, TN, data):
         if buf is None:
             return None
-        if buf.numel() != TN * data.shape[-1] * data.shape[-2] or not buf.is_contiguous():
-            raise ValueError(f"{name} must be a contiguous [numH,numW,N,H*W] buffer")
+        row = cls.rate_row(data.shape[-2], data.shape[-1])
+        if buf.numel() != TN * row or not buf.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous [numH,numW,N,{row}] buffer")
         return _hip.dev_f32(buf, name)
 
     def run(self, data, counts, locs, fluxes, temperature, log_target=None, *, prior=None,
@@ -162,6 +170,12 @@ class SingleComponentMH(object):
         off = self.rng.take(self.num_iters)
         if tail is not None and tail_take:
             tail.offset = self.rng.take(tail_take)
+        if (self._entry == "smcdet_mh_sweep" and rate_out is None
+                and data.shape[-1] * data.shape[-2] > _hip.MAX_TILE_PIXELS):
+            # tiles above the LDS budget: the sweep needs working rate images
+            rate_out = torch.empty(T * N * self.rate_row(data.shape[-2], data.shape[-1]),
+                                   device=dev, dtype=torch.float32)
+            rate_in = None
         cm, cp, ch = image_model._cmodel(), prior._cprior(), self._cmh(prior)
         extra_flags = flags
         flags = (_hip.SMCDET_MH_FULL_RECOMPUTE if self.full_recompute else 0) | self.debug_flags

@@ -44,9 +44,17 @@ class SMCsampler(object):
         # anything touches the device)
         nt = (image.shape[0] * image.shape[1] if image.dim() == 4
               else (image.shape[0] // tile_dim) ** 2)
+        # tiles above the LDS budget: SingleComponentMH sweeps with the M71
+        # image model run from global memory
+        from .images import M71ImageModel
+        from .kernel import SingleComponentMALA, SingleComponentMH
+        global_ok = (isinstance(MutationKernel, SingleComponentMH)
+                     and not isinstance(MutationKernel, SingleComponentMALA)
+                     and isinstance(ImageModel, M71ImageModel))
         _hip.check_limits(tile_dim, tile_dim, Prior.max_objects,
                           self._particles_per_tile(Prior, num_catalogs), nt,
-                          getattr(ImageModel, "psf_radius", None), where="SMCsampler")
+                          getattr(ImageModel, "psf_radius", None), where="SMCsampler",
+                          global_ok=global_ok)
         if device is None:
             device = image.device if image.is_cuda else torch.device(
                 "cuda", torch.cuda.current_device())
@@ -260,7 +268,8 @@ class SMCsampler(object):
         """(rate_in, rate_out) for the next sweep, or (None, None)."""
         if not self.persist_rate_images or getattr(self.MutationKernel, "full_recompute", False):
             return None, None
-        shape = (*self.locs.shape[:3], self.tile_dim * self.tile_dim)
+        shape = (*self.locs.shape[:3],
+                 self.MutationKernel.rate_row(self.tile_dim, self.tile_dim))
         for i in (0, 1):
             if self._rate[i] is None or tuple(self._rate[i].shape) != shape:
                 self._rate[i] = torch.empty(shape, device=self.device, dtype=torch.float32)

@@ -65,10 +65,19 @@ def test_invalid_arguments_fail_loudly_without_gpu():
     assert rc == -1
     assert b"null" in L.smcdet_last_error()
     m = _hip.ImageModelC()
-    m.model, m.H, m.W, m.psf_radius = 1, 100, 100, 8  # 10,000 px > 4,096
+    m.model, m.H, m.W, m.psf_radius = 1, 300, 300, 8  # 90,000 px > 65,536
     rc = L.smcdet_loglik(ctypes.byref(m), ctypes.c_void_p(1), ctypes.c_void_p(1),
                          ctypes.c_void_p(1), 1, 1, 1, ctypes.c_void_p(1), None)
     assert rc == -2
+    # above 4,096 px only the M71 model has the global-memory paths
+    m.model, m.H, m.W = 2, 100, 100
+    rc = L.smcdet_loglik(ctypes.byref(m), ctypes.c_void_p(1), ctypes.c_void_p(1),
+                         ctypes.c_void_p(1), 1, 1, 1, ctypes.c_void_p(1), None)
+    assert rc == -2 and b"M71" in L.smcdet_last_error()
+    # the LDS-resident kernels (MALA, MCMC chains, aggregation) keep 4,096 px
+    m.model = 1
+    rc = L.smcdet_mala_sweep(ctypes.byref(m), *([0] * 25))
+    assert rc in (-1, -2)
     with pytest.raises(RuntimeError, match="failed"):
         _hip.check(rc, "smcdet_loglik")
 

@@ -83,13 +83,22 @@ def test_unsupported_shapes_fail_at_construction():
                          pad=4)
         return model, prior
 
+    from smcdet_amd.kernel import SingleComponentMALA
     mh = SingleComponentMH(10, 0.1, 2.5, 0.06, 1800.0)
     img = torch.zeros(128, 128)
     model, prior = make(128, 10)
+    # SMC with SingleComponentMH and the M71 model runs tiles up to 256x256
+    # (global-memory sweep); MALA and the MCMC chains keep
+    # the LDS budget
     with pytest.raises(ValueError, match="16384 pixels.*4096"):
-        SMCsampler(img, 128, prior, model, mh, 512, 0.5, "systematic", 0.25, 10)
+        SMCsampler(img, 128, prior, model, SingleComponentMALA(10, 0.1, 2.5, 0.06, 1800.0), 512,
+                   0.5, "systematic", 0.25, 10)
     with pytest.raises(ValueError, match="4096"):
         MHsampler(img, 128, prior, model, 0.1, 2.5, 0.25, 100, 10)
+    model, prior = make(300, 10)
+    with pytest.raises(ValueError, match="90000 pixels.*65536"):
+        SMCsampler(torch.zeros(300, 300), 300, prior, model, mh, 512, 0.5, "systematic", 0.25,
+                   10)
     model, prior = make(32, 80)
     with pytest.raises(ValueError, match="max_objects = 80 > 64"):
         SMCsampler(torch.zeros(32, 32), 32, prior, model, mh, 512, 0.5, "systematic", 0.25, 10)
