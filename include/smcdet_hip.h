@@ -171,7 +171,11 @@ int smcdet_launch_timing_read(float* ms, int32_t max, int32_t* n_out);
 int smcdet_launch_timing_starts(float* ms, int32_t max, int32_t* n_out);
 
 /* ImageModel.loglikelihood / M71ImageModel.loglikelihood
- * (smcdet/images.py:85-102, :159-175): out[T,N]. */
+ * (smcdet/images.py:85-102, :159-175): out[T,N].  Tiles up to 4096 pixels
+ * (either model) stage the tile in LDS; M71 tiles up to 65536 pixels render
+ * 64-pixel chunks in registers and read the tile from global memory
+ * (smcdet_render likewise).  MALA, MCMC chains and aggregation sweeps keep
+ * the 4096-pixel LDS budget. */
 int smcdet_loglik(const smcdet_image_model_t* model, const float* tiled_image,
                   const float* locs, const float* fluxes, int32_t T, int32_t N,
                   int32_t S, float* out, void* stream);
@@ -233,6 +237,13 @@ int smcdet_prior_sample(const smcdet_prior_t* prior, int32_t T,
  * rate_out receives the image of the returned state (maintained
  * incrementally, float32 update rounding).  rate_in must describe *_in
  * exactly; rate_in != rate_out when ancestors is non-null.
+ * Tiles above 4096 pixels (M71 model, up to 65536 = 256x256 pixels): the tile
+ * image and the rate images live in global memory -- rate_in / rate_out are
+ * [T,N,H*W+64] (64 dummy cells per row for masked lanes), rate_out is
+ * REQUIRED (the sweep updates its rows in place; with FULL_RECOMPUTE their
+ * contents afterwards are unspecified), rate_in == rate_out is allowed
+ * without ancestors, and the fused step (smcdet_mh_sweep_step) runs as two
+ * launches.
  * go (nullable, int32 device scalar): when *go == 0 the launch does nothing
  * (no output is written) -- lets a host enqueue the next SMC iteration before
  * it has read the loop condition (see smcdet_temper_reweight's `live`).
@@ -434,7 +445,7 @@ int smcdet_prune(const float* locs, const float* fluxes, int32_t T, int32_t N,
                  void* stream);
 
 /* ---- tile aggregation (smcdet/aggregate.py:8-593, Aggregate) ------------- */
-#define SMCDET_AGG_MAX_SOURCES 256
+#define SMCDET_AGG_MAX_SOURCES 4096
 
 /* Aggregate.mutate (aggregate.py:176-187 with log_target :105-130): K =
  * mh->num_iters single-component MH iterations on joint tiles of
@@ -452,7 +463,12 @@ int smcdet_prune(const float* locs, const float* fluxes, int32_t T, int32_t N,
  * state).  acc_rate [T] (nullable) = acceptance rate of the last iteration,
  * with acc_count [2T] as in smcdet_mh_sweep.  Replay layout as
  * smcdet_mh_replay_t (comp must be < count).  tile_boxes (nullable): per
- * joint tile location boxes in place of mh->locs_min/max. */
+ * joint tile location boxes in place of mh->locs_min/max.
+ * workspace (nullable): joint tiles whose image, two rate images and catalog
+ * per wave do not fit LDS at 4 waves per workgroup (smcdet_aggregate_workspace
+ * > 0; M71 model, up to 65536 pixels and 4096 sources) keep them in this
+ * caller-owned device buffer of smcdet_aggregate_workspace() floats and read
+ * the tile image from global memory. */
 int smcdet_aggregate_sweep(const smcdet_image_model_t* model,
                            const smcdet_prior_t* prior, const smcdet_mh_t* mh,
                            int32_t axis, const float* tiled_image,
@@ -464,7 +480,11 @@ int smcdet_aggregate_sweep(const smcdet_image_model_t* model,
                            uint64_t offset, const smcdet_mh_replay_t* replay,
                            float* loglik_parent, float* loglik_children,
                            float* acc_rate, int32_t* acc_count,
-                           const float* tile_boxes, void* stream);
+                           const float* tile_boxes, float* workspace, void* stream);
+/* Floats of workspace smcdet_aggregate_sweep needs for these shapes (0: the
+ * LDS path runs; < 0: unsupported, smcdet_last_error says why). */
+int64_t smcdet_aggregate_workspace(const smcdet_image_model_t* model, int32_t T,
+                                   int32_t N, int32_t S);
 
 /* Aggregate.temper (aggregate.py:140-174), per count group: the particles of
  * each joint tile are sorted by count and split into G segments (count

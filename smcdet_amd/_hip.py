@@ -37,7 +37,7 @@ MAX_SOURCES = 64            # S = Prior.max_objects: one source per lane
 MAX_PARTICLES = 16384       # N per tile: the tile kernel holds 32 log-likelihoods per thread
 MAX_TILES = 65535           # T: the MH grid's y dimension
 MAX_PSF_RADIUS = 64
-MAX_AGG_SOURCES = 256       # sources of an aggregated (joint) tile: catalog in LDS
+MAX_AGG_SOURCES = 4096      # sources of an aggregated (joint) tile (LDS or workspace catalog)
 
 
 def check_limits(H, W, S, N=None, T=None, R=None, where="sampler", global_ok=False):
@@ -147,8 +147,9 @@ _SIGS = {
                                 c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
     "smcdet_prune": ([c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p, c_p, c_p, c_p], c_i),
     "smcdet_aggregate_sweep": ([c_p, c_p, c_p, c_i, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p,
-                                c_p, c_p, c_p, c_u64, c_u64, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
-                               c_i),
+                                c_p, c_p, c_p, c_u64, c_u64, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                                c_p], c_i),
+    "smcdet_aggregate_workspace": ([c_p, c_i, c_i, c_i], c_i64),
     "smcdet_aggregate_temper": ([c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_d, c_p, c_p],
                                 c_i),
     "smcdet_aggregate_reweight": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p,

@@ -191,14 +191,21 @@ def aggregate_sweep(image_model, prior, mh, axis, data, temperature, counts, loc
         ancestors = ancestors.to(device=dev, dtype=torch.int64).contiguous()
     if tile_boxes is not None:
         tile_boxes = _hip.dev_f32(tile_boxes.to(dev), "tile_boxes")
+    cm = image_model._cmodel()
+    # joint tiles beyond the LDS budget: rate images and catalog per particle in
+    # a device workspace (the global-memory sweep, M71)
+    need = int(_hip.lib().smcdet_aggregate_workspace(_hip.ref(cm), T, N, S))
+    if need < 0:
+        _hip.check(need, "smcdet_aggregate_workspace")
+    work = torch.empty(need, device=dev, dtype=torch.float32) if need > 0 else None
     _hip.check(_hip.lib().smcdet_aggregate_sweep(
-        _hip.ref(image_model._cmodel()), _hip.ref(prior._cprior()), _hip.ref(ch), int(axis),
+        _hip.ref(cm), _hip.ref(prior._cprior()), _hip.ref(ch), int(axis),
         _hip.ptr(data), _hip.ptr(temperature), T, N, S, _hip.ptr(ancestors), _hip.ptr(counts),
         _hip.ptr(locs), _hip.ptr(fluxes), _hip.ptr(co), _hip.ptr(lo), _hip.ptr(lf), int(seed),
         int(offset), _hip.ref(rp) if rp is not None else None, _hip.ptr(lp), _hip.ptr(lc),
-        _hip.ptr(acc), _hip.ptr(acc_workspace), _hip.ptr(tile_boxes), _hip.stream_of(lo)),
-        "smcdet_aggregate_sweep")
-    del keep
+        _hip.ptr(acc), _hip.ptr(acc_workspace), _hip.ptr(tile_boxes), _hip.ptr(work),
+        _hip.stream_of(lo)), "smcdet_aggregate_sweep")
+    del keep, work
     return co, lo, lf, lp, lc, acc
 
 
@@ -292,9 +299,12 @@ class Aggregate(object):
                              f"{self.numH}x{self.numW} (aggregate.py:40)")
         self.num_aggregation_levels = int(round(2 * math.log2(self.numH)))
         fh, fw = self.numH * self.dimH, self.numW * self.dimW
-        if fh * fw > _hip.MAX_TILE_PIXELS:
-            raise ValueError(f"Aggregate: the aggregated {fh}x{fw} image exceeds "
-                             f"{_hip.MAX_TILE_PIXELS} pixels (the joint tile lives in LDS)")
+        # joint tiles beyond the LDS budget run the global-memory sweep (M71)
+        from .images import M71ImageModel
+        limit = (_hip.MAX_TILE_PIXELS_GLOBAL if isinstance(ImageModel, M71ImageModel)
+                 else _hip.MAX_TILE_PIXELS)
+        if fh * fw > limit:
+            raise ValueError(f"Aggregate: the aggregated {fh}x{fw} image exceeds {limit} pixels")
         lnc = torch.as_tensor(log_normalizing_constant, dtype=torch.float32)
         if lnc.dim() != 2 or tuple(lnc.shape) != (self.numH, self.numW):
             raise ValueError("log_normalizing_constant must be [numH, numW]")

@@ -71,6 +71,7 @@ struct AggArgs {
   const float* r_uloc;
   const float* r_uflux;
   const float* r_uacc;
+  float* work;         // GL: per-particle [2*H*W + 3*S] scratch (rate images, catalog)
 };
 
 // Both rate images from the LDS catalog: lamP = B + sum_s g f_s psf_s,
@@ -131,7 +132,9 @@ __device__ __forceinline__ void agg_position(const AggArgs& a, int ph, int pw, f
   dlC = (pside == side_n ? vn : 0.f) - (pside == side_o ? vo : 0.f);
 }
 
-template <int MODEL, bool REPLAY>
+// GL: joint tiles above the LDS budget -- tile image read from global memory,
+// both rate images and the catalog in the caller's workspace (row per particle)
+template <int MODEL, bool REPLAY, bool GL = false>
 __global__ __launch_bounds__(kAggMaxWaves* kWave) void agg_sweep_kernel(AggArgs a) {
   extern __shared__ float smem[];
   __shared__ int wg_acc, wg_done;
@@ -147,8 +150,12 @@ __global__ __launch_bounds__(kAggMaxWaves* kWave) void agg_sweep_kernel(AggArgs 
   float* lamP = smem + kImg * HWp + wave * per_wave;
   float* lamC = lamP + HWp;
   float* cat = lamC + HWp;
-
-  stage_image<MODEL>(a.img + (size_t)t * HW, xs, lg, HW, threadIdx.x, a.nw * kWave);
+  if constexpr (GL) {
+    xs = const_cast<float*>(a.img) + (size_t)t * HW;
+    lg = nullptr;
+  } else {
+    stage_image<MODEL>(a.img + (size_t)t * HW, xs, lg, HW, threadIdx.x, a.nw * kWave);
+  }
   if (threadIdx.x == 0) {
     wg_acc = 0;
     wg_done = 0;
@@ -160,6 +167,11 @@ __global__ __launch_bounds__(kAggMaxWaves* kWave) void agg_sweep_kernel(AggArgs 
   const int N = a.N, S = a.S;
   const size_t pid = (size_t)t * N + n;
   const size_t src = a.ancestors ? (size_t)t * N + (size_t)a.ancestors[pid] : pid;
+  if constexpr (GL) {
+    lamP = a.work + pid * (2 * (size_t)HW + 3 * (size_t)S);
+    lamC = lamP + HW;
+    cat = lamC + HW;
+  }
   const float count = a.counts_in[src];
   if (a.counts_out && lane == 0) a.counts_out[pid] = count;
   const int Sj = min(max((int)count, 0), S);
@@ -323,6 +335,23 @@ __global__ __launch_bounds__(kAggMaxWaves* kWave) void agg_sweep_kernel(AggArgs 
 
 using namespace smcdet;
 
+extern "C" int64_t smcdet_aggregate_workspace(const smcdet_image_model_t* model, int32_t T,
+                                              int32_t N, int32_t S) {
+  int rc = validate_model(model, kMaxGlobalPixels);
+  if (rc) return rc;
+  if (T <= 0 || N <= 0 || T > 65535) return set_error(SMCDET_EUNSUPPORTED, "T=%d N=%d", T, N);
+  if (S < 1 || S > SMCDET_AGG_MAX_SOURCES)
+    return set_error(SMCDET_EUNSUPPORTED, "S=%d outside 1..%d", S, SMCDET_AGG_MAX_SOURCES);
+  const size_t HWp = (size_t)model->H * model->W + kWave;
+  const size_t img_b = (model->model == SMCDET_MODEL_POISSON ? 2 : 1) * HWp * sizeof(float);
+  const size_t wave_b = (2 * HWp + 3 * (size_t)S) * sizeof(float);
+  if (img_b + kAggMaxWaves * wave_b <= 160 * 1024) return 0;  // LDS path
+  if (model->model != SMCDET_MODEL_M71)
+    return set_error(SMCDET_EUNSUPPORTED, "joint tile %dx%d with S=%d exceeds LDS (M71 only "
+                     "beyond)", model->H, model->W, S);
+  return (int64_t)T * N * (2 * (int64_t)model->H * model->W + 3 * (int64_t)S);
+}
+
 extern "C" int smcdet_aggregate_sweep(
     const smcdet_image_model_t* model, const smcdet_prior_t* prior, const smcdet_mh_t* mh,
     int32_t axis, const float* tiled_image, const float* temperature, int32_t T, int32_t N,
@@ -330,22 +359,23 @@ extern "C" int smcdet_aggregate_sweep(
     const float* fluxes_in, float* counts_out, float* locs_out, float* fluxes_out, uint64_t seed,
     uint64_t offset, const smcdet_mh_replay_t* replay, float* loglik_parent,
     float* loglik_children, float* acc_rate, int32_t* acc_count, const float* tile_boxes,
-    void* stream) {
-  int rc = validate_model(model);
-  if (rc) return rc;
-  rc = validate_prior(prior);
+    float* workspace, void* stream) {
+  const int64_t need = smcdet_aggregate_workspace(model, T, N, S);
+  if (need < 0) return (int)need;
+  int rc = validate_prior(prior);
   if (rc) return rc;
   if (!mh) return set_error(SMCDET_EINVAL, "mh params are null");
   if (!tiled_image || !temperature || !counts_in || !locs_in || !fluxes_in || !locs_out ||
       !fluxes_out)
     return set_error(SMCDET_EINVAL, "null buffer");
+  const bool gl = need > 0;
+  if (gl && !workspace)
+    return set_error(SMCDET_EINVAL, "joint tile %dx%d with S=%d needs a workspace of %lld floats",
+                     model->H, model->W, S, (long long)need);
   if (acc_rate && !acc_count) return set_error(SMCDET_EINVAL, "acc_rate needs acc_count");
   if (axis != 0 && axis != 1) return set_error(SMCDET_EINVAL, "axis %d not 0 or 1", axis);
   const int dim = axis == 0 ? model->H : model->W;
   if (dim % 2) return set_error(SMCDET_EUNSUPPORTED, "joint tile side %d is odd", dim);
-  if (T <= 0 || N <= 0 || T > 65535) return set_error(SMCDET_EUNSUPPORTED, "T=%d N=%d", T, N);
-  if (S < 1 || S > SMCDET_AGG_MAX_SOURCES)
-    return set_error(SMCDET_EUNSUPPORTED, "S=%d outside 1..%d", S, SMCDET_AGG_MAX_SOURCES);
   if (mh->num_iters < 0) return set_error(SMCDET_EINVAL, "num_iters < 0");
   if (!(mh->locs_stdev > 0.f) || !(mh->fluxes_stdev > 0.f))
     return set_error(SMCDET_EINVAL, "proposal standard deviations must be > 0");
@@ -398,20 +428,26 @@ extern "C" int smcdet_aggregate_sweep(
     a.r_uflux = replay->uflux;
     a.r_uacc = replay->uacc;
   }
-  // waves per workgroup: as many as fit the 160 KiB LDS (image + per wave two
-  // rate images and the catalog)
+  a.work = workspace;
+  hipStream_t st = (hipStream_t)stream;
+  if (gl) {  // M71 (smcdet_aggregate_workspace), 4 waves, no dynamic LDS
+    a.nw = kAggMaxWaves;
+    const dim3 grid((N + a.nw - 1) / a.nw, T), block(a.nw * kWave);
+    if (replay)
+      hipLaunchKernelGGL((agg_sweep_kernel<SMCDET_MODEL_M71, true, true>), grid, block, 0, st, a);
+    else
+      hipLaunchKernelGGL((agg_sweep_kernel<SMCDET_MODEL_M71, false, true>), grid, block, 0, st, a);
+    return check_launch("smcdet_aggregate_sweep");
+  }
+  // 4 waves per workgroup (smcdet_aggregate_workspace sends joint tiles that
+  // do not fit at 4 waves to the global-memory path)
   const size_t HWp = (size_t)model->H * model->W + kWave;
   const size_t img_b = (model->model == SMCDET_MODEL_POISSON ? 2 : 1) * HWp * sizeof(float);
   const size_t wave_b = (2 * HWp + 3 * (size_t)S) * sizeof(float);
-  int nw = kAggMaxWaves;
-  while (nw > 1 && img_b + nw * wave_b > 160 * 1024) --nw;
+  const int nw = kAggMaxWaves;
   const size_t lds = img_b + nw * wave_b;
-  if (lds > 160 * 1024)
-    return set_error(SMCDET_EUNSUPPORTED, "joint tile %dx%d with S=%d needs %zu B of LDS",
-                     model->H, model->W, S, lds);
   a.nw = nw;
   const dim3 grid((N + nw - 1) / nw, T), block(nw * kWave);
-  hipStream_t st = (hipStream_t)stream;
   const bool m71 = a.m.model == SMCDET_MODEL_M71;
   const void* fn =
       replay ? (m71 ? (const void*)agg_sweep_kernel<SMCDET_MODEL_M71, true>
