@@ -37,3 +37,28 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all clean oracle trace
+
+# host sanitizer builds: the C oracle and the library's host side
+# (-Xarch_host -fsanitize=..., device code not compiled: nothing is launched)
+# with drivers that run without a GPU (tests/test_sanitizers.py)
+ASAN_DIR := build/asan
+ASAN_FLAGS := -fsanitize=address,undefined -fno-omit-frame-pointer -g -O1
+asan: $(ASAN_DIR)/oracle_driver $(ASAN_DIR)/capi_driver
+
+$(ASAN_DIR)/oracle_driver: scripts/asan/oracle_driver.c oracle/mh_oracle.c
+	mkdir -p $(ASAN_DIR)
+	gcc $(ASAN_FLAGS) -fopenmp -std=c11 -o $@ scripts/asan/oracle_driver.c -lm
+
+ASAN_HIP := $(HIPCC) -std=c++17 -O1 -g --offload-arch=$(ARCH) -Xarch_host -fsanitize=address \
+  -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer
+ASAN_OBJS := $(patsubst $(CSRC)/%.hip,$(ASAN_DIR)/%.o,$(SRCS))
+$(ASAN_DIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	mkdir -p $(ASAN_DIR)
+	$(ASAN_HIP) -c $< -o $@
+$(ASAN_DIR)/capi_driver.o: scripts/asan/capi_driver.cpp include/smcdet_hip.h
+	mkdir -p $(ASAN_DIR)
+	$(ASAN_HIP) -c $< -o $@
+$(ASAN_DIR)/capi_driver: $(ASAN_DIR)/capi_driver.o $(ASAN_OBJS)
+	$(ASAN_HIP) -o $@ $^
+
+.PHONY: asan

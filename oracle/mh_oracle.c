@@ -11,7 +11,9 @@
  * MH draws, and (b) as bench.py's `cpu_baseline` ("port") on the GPU box's
  * host cores.  Never linked into the product library.
  */
+#ifndef _GNU_SOURCE
 #define _GNU_SOURCE
+#endif
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>

@@ -317,3 +317,63 @@ def test_aggregate_partition_boxes_evidence_matches():
     assert abs(m["agg_lz"] - m["big_lz"]) < 5.0, m
     assert abs(m["agg_count"] - m["big_count"]) < count_tol(m, 0.6), m
     assert abs(m["agg_flux"] / m["big_flux"] - 1) < 0.03, m
+
+
+def _moderate_32():
+    """The c2_moderate 32x32 M71 image's stars (make_golden.py:
+    c2_moderate_truth_image): four stars of 2-12 nmgy and a faint one."""
+    torch.manual_seed(72)
+    l = torch.tensor([[[[[7.3, 9.6], [21.8, 6.2], [15.1, 24.7], [26.4, 27.9], [4.2, 22.5]]]]],
+                     device=DEV)
+    f = torch.tensor([[[[12.0, 6.0, 4.0, 2.0, 0.8]]]], device=DEV)
+    return p_model(32, 32).sample(l, f)[0, 0, :, :, 0].contiguous()
+
+
+def test_aggregate_bench_geometry_vs_single_tile():
+    """VERDICT r2 next #8, the bench's aggregation geometry: CS-SMC on the 4x4
+    8x8 tiles of a 32x32 image (counts 0..6 per tile, pad_mode "partition",
+    pad 2), Aggregate over 4 levels to one 32x32 population, against CS-SMC on
+    the whole 32x32 tile (counts 0..12, the same Poisson prior per pixel), 6
+    seeds each, N = 4096 per count, K = 100: log evidence within 1% (and the
+    difference reported in pooled SE), the posterior mean number of detectable
+    stars and their total flux within 3 pooled SE (floors 0.5 stars, 3%)."""
+    from smcdet_amd.aggregate import Aggregate
+    from smcdet_amd.cssmc import CountStratifiedSMC
+    thr = M71["flux_detection_threshold"]
+    img = _moderate_32()
+    N, K, rate, pad = 4096, 100, 0.003125, 2
+    rows = []
+    for seed in range(6):
+        kp = p_prior(8, 8, 0, 6, rate, pad, "partition")
+        kids = CountStratifiedSMC(img, 8, kp, p_model(8, 8), mh(K), N, 0.5, "systematic", thr, 300,
+                                  print_every=10 ** 9, num_catalogs=N, seed=400 + seed)
+        _quiet(kids.run)
+        agg = Aggregate(kp, p_model(8, 8), mh(K), kids.tiled_image, kids.counts, kids.locs,
+                        kids.fluxes, kids.weights, kids.log_normalizing_constant, thr,
+                        "systematic", 0.5, print_every=10 ** 9, seed=500 + seed)
+        _quiet(agg.run)
+        assert agg.num_aggregation_levels == 4
+        big = CountStratifiedSMC(img, 32, p_prior(32, 32, 0, 12, rate, pad, "partition"),
+                                 p_model(32, 32), mh(K), N, 0.5, "systematic", thr, 300,
+                                 print_every=10 ** 9, num_catalogs=N, seed=600 + seed)
+        _quiet(big.run)
+        rows.append(dict(
+            agg_lz=float(agg.log_evidence.reshape(-1)[0]),
+            big_lz=float(big.log_normalizing_constant.reshape(-1)[0]),
+            agg_count=float(agg.pruned_counts.float().mean()),
+            big_count=float(big.pruned_counts.float().mean()),
+            agg_flux=float(agg.pruned_fluxes.sum(-1).mean()),
+            big_flux=float(big.pruned_fluxes.sum(-1).mean())))
+    print(rows)
+    m = {k: float(np.mean([r[k] for r in rows])) for k in rows[0]}
+
+    def pooled(a, b):
+        return float(np.hypot(*(np.std([r[k] for r in rows], ddof=1) / np.sqrt(len(rows))
+                                for k in (a, b))))
+
+    se_lz = pooled("agg_lz", "big_lz")
+    print("mean", m, "lz pooled SE", se_lz)
+    assert abs(m["agg_lz"] - m["big_lz"]) < 0.01 * abs(m["big_lz"]), (m, se_lz)
+    assert abs(m["agg_count"] - m["big_count"]) < max(0.5, 3 * pooled("agg_count", "big_count")), m
+    assert abs(m["agg_flux"] - m["big_flux"]) < max(0.03 * m["big_flux"],
+                                                    3 * pooled("agg_flux", "big_flux")), m
