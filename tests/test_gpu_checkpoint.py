@@ -98,3 +98,40 @@ def test_progress_lines_match_synchronous_loop():
         last = s.iter
     assert outs[0] == outs[1]
     assert len(outs[0]) == last // 2
+
+
+def test_fused_resume_from_unfused_checkpoint():
+    """a checkpoint taken from a fused=False run carries no pending
+    resampling indices; loading it into a fused sampler draws them from the
+    restored weights at the stream offset the unfused resample() would use,
+    so the resumed fused run ends exactly where the uninterrupted unfused run
+    does (rate images off in both: the fused and unfused schedules then
+    consume the same draws in the same order)."""
+    from smcdet_amd.sampler import SMCsampler
+    img = _image()
+
+    def make(fused, seed=5):
+        return SMCsampler(img, H, p_m71_prior(H, S, S), p_m71_model(H), p_m71_mh(K), N, 0.5,
+                          "systematic", M71["flux_detection_threshold"], 200,
+                          print_every=10 ** 9, seed=seed, fused=fused, persist_rate_images=False)
+
+    saved = {}
+    a = make(False)
+
+    def hook(s):
+        if s.iter == 4:
+            saved["st"] = s.state_dict(with_rate_images=False)
+
+    a.on_iteration = hook
+    with contextlib.redirect_stdout(io.StringIO()):
+        a.run()
+    st = saved["st"]
+    assert "_pending_idx" not in st
+    b = make(True, seed=999)
+    b.load_state_dict(st)
+    assert b._pending_idx is not None
+    with contextlib.redirect_stdout(io.StringIO()):
+        b.resume()
+    assert b.iter == a.iter
+    for k in ("log_normalizing_constant", "temperature", "pruned_counts", "locs", "fluxes"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k

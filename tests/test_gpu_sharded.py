@@ -282,3 +282,52 @@ def test_c3_full_size_lockstep():
     two.run()
     for f in FIELDS:
         assert torch.equal(flat_tiles(two, f), flat_tiles(ind, f)[:2]), f
+
+
+def test_partition_boxes_follow_the_grid_in_shards_and_batches():
+    """with pad_mode="partition" a rank's tiles keep the
+    location boxes of their places in the whole image's grid (not of the flat
+    1 x T_local launch grid), so a sharded run equals the single-process run
+    tile for tile; BatchSMC gives every independent image the full padded box
+    (a 1x1 grid's partition)."""
+    from smcdet_amd._rng import rank_seed
+    from smcdet_amd.batch import BatchSMC
+    from smcdet_amd.prior import M71Prior, partition_boxes
+    from smcdet_amd.sampler import SMCsampler
+
+    def prior():
+        return M71Prior(min_objects=S, max_objects=S, counts_rate=0.003125, image_height=H,
+                        image_width=H, flux_alpha=M71["flux_alpha"], flux_lower=M71["flux_lower"],
+                        flux_upper=M71["flux_upper"], pad=4, pad_mode="partition")
+
+    img = grid_image(3, seed=12)            # 3x3 tiles: middle tiles have no padding
+    args = (p_m71_model(H), p_m71_mh(K), N, 0.5, "systematic", M71["flux_detection_threshold"],
+            300)
+    single = SMCsampler(img, H, prior(), *args, print_every=10 ** 9, seed=61,
+                        stopping="independent")
+    single.run()
+    boxes = partition_boxes((3, 3), H, H, 4, "cuda")
+    assert torch.equal(single.tile_boxes, boxes)
+    for rank in range(2):
+        from smcdet_amd.distributed import TileShardedSMC
+        sh = TileShardedSMC(img, H, prior(), *args, seed=61, rank=rank, world_size=2,
+                            stopping="independent")
+        assert torch.equal(sh.sampler.tile_boxes, boxes[sh.start:sh.stop]), rank
+        sh.run()
+        if rank == 0:
+            for f in FIELDS:
+                assert torch.equal(flat_tiles(sh.sampler, f),
+                                   flat_tiles(single, f)[sh.start:sh.stop]), f
+        else:
+            tiles = img.unfold(0, H, H).unfold(1, H, H).reshape(1, 9, H, H)
+            alone = SMCsampler.from_tiles(tiles[:, sh.start:sh.stop].contiguous(), prior(), *args,
+                                          print_every=10 ** 9, seed=rank_seed(61, 1),
+                                          stopping="independent",
+                                          tile_boxes=boxes[sh.start:sh.stop])
+            alone.run()
+            for f in FIELDS:
+                assert torch.equal(flat_tiles(sh.sampler, f), flat_tiles(alone, f)), f
+    b = BatchSMC(img.unfold(0, H, H).unfold(1, H, H).reshape(9, H, H)[:3].contiguous(), prior(),
+                 *args)
+    full = partition_boxes((1, 1), H, H, 4, "cuda")
+    assert torch.equal(b.sampler.tile_boxes, full.repeat(3, 1))
