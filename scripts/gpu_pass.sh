@@ -9,7 +9,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-STEPS=${STEPS:-"pytest smoke bench torchrun1 profile large"}
+STEPS=${STEPS:-"pytest smoke bench torchrun1 host profile large"}
 step() {
   echo "$1 rc=$2"
   if [ "$2" -ne 0 ] && [ "$2" -ne 1 ]; then echo "stopping after $1"; exit "$2"; fi
@@ -38,12 +38,21 @@ if has torchrun1; then
   step torchrun1 $?
   tail -c 400 gpurun_out/bench_torchrun1.log; echo
 fi
+if has host; then  # host-side issue cost of a step vs its GPU time
+  timeout -k 10 200 python scripts/host_overhead.py > gpurun_out/host_overhead.json 2>gpurun_out/host_overhead.err
+  step host $?
+  cat gpurun_out/host_overhead.json
+fi
 if has profile; then
   OUT=gpurun_out/prof SUMMARY=gpurun_out/pmc_mh_r03.json \
     SQ="SQ_INSTS_VALU SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP32_TRANS SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_INSTS_SMEM" \
     bash scripts/profile.sh
   step profile $?
   cat gpurun_out/prof/summary.txt | tail -20
+  tr=$(find gpurun_out/prof/trace -name 'run_kernel_trace.csv' | head -1)
+  if [ -n "$tr" ]; then
+    python scripts/step_attribution.py "$tr" --json gpurun_out/step_attribution.json | tail -8
+  fi
 fi
 if has large; then  # the global-memory (large-tile) paths, last
   timeout -k 10 300 python -u -m pytest tests/test_gpu_large_tile.py -v -p no:cacheprovider \
