@@ -194,8 +194,9 @@ def test_tile_pass_4096_vs_reference():
     # (1) reweighting at the reference's temperatures
     lw, W = torch.empty_like(ll), torch.empty_like(ll)
     ess, lz = T(np.zeros(n, np.float32)), T(lz_in)
+    t_out, t_in = T(tau_out), T(tau_in)  # (bound: the call only sees raw pointers)
     _hip.check(_hip.lib().smcdet_update_weights(
-        _hip.ptr(ll), _hip.ptr(T(tau_out)), _hip.ptr(T(tau_in)), _hip.ptr(lw), _hip.ptr(W),
+        _hip.ptr(ll), _hip.ptr(t_out), _hip.ptr(t_in), _hip.ptr(lw), _hip.ptr(W),
         _hip.ptr(ess), _hip.ptr(lz), n, Np, _hip.stream_of(ll)), "update_weights")
     np.testing.assert_allclose(N(W), np.stack([c["W"] for c in cases]), rtol=1e-5, atol=1e-12)
     np.testing.assert_allclose(N(ess), [float(c["ess"]) for c in cases], rtol=1e-5)
@@ -239,8 +240,9 @@ def _resample_idx(W, U):
     W = T(W)
     nH, nW, Np = W.shape
     idx = torch.empty(W.shape, device=DEV, dtype=torch.int64)
+    u = T(U)
     _hip.check(_hip.lib().smcdet_resample_index(
-        _hip.ptr(W), nH * nW, Np, _hip.SMCDET_RESAMPLE_SYSTEMATIC, 0, 0, _hip.ptr(T(U)),
+        _hip.ptr(W), nH * nW, Np, _hip.SMCDET_RESAMPLE_SYSTEMATIC, 0, 0, _hip.ptr(u),
         _hip.ptr(idx), _hip.stream_of(W)), "resample_index")
     return N(idx)
 
