@@ -522,7 +522,7 @@ def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
     return out
 
 
-def vs_reference(dev, which="c2_moderate", n_runs=48):
+def vs_reference(dev, which="c2_moderate", n_runs=128):
     """North-star parity at the headline geometry, outside the timed region:
     the reference's recorded runs (tests/golden/stats_<which>.json: one 32x32
     M71 tile, S=10, N=4096 or 512, K=20, systematic, >= 20 seeds) against n_runs runs
