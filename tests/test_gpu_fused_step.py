@@ -67,7 +67,10 @@ def _assert_same(a, b):
 @pytest.mark.parametrize("N", [4096, 1024, 512])
 def test_fused_step_equals_split_step_c2(N):
     """C2 geometry (one 32x32 tile, S = 10, K = 100): every output of 6 SMC
-    iterations is identical for the fused and the two-launch step."""
+    iterations is identical for the fused and the two-launch step.  A
+    self-consistency regression, not parity evidence (the reference parity
+    of the tile pass at N = 4096 is test_gpu_parity.py::
+    test_tile_pass_4096_vs_reference)."""
     from smcdet_amd import _hip
     img = _image(32, 5)
     a = _sampler(img, 32, N, 10, 100, 77, fused_step=True)

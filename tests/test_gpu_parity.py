@@ -404,7 +404,9 @@ def test_smc_end_to_end_replay_vs_reference(name, fused):
 def test_mh_incremental_matches_full_recompute_c2():
     """Same Philox streams, C2 geometry: the incremental delta-likelihood sweep
     and the full re-render sweep (reference arithmetic) make the same moves
-    except for rare near-tie decisions."""
+    except for rare near-tie decisions.  A self-consistency regression, not
+    parity evidence: decision parity with the reference at this geometry is
+    tests/test_gpu_teacher.py (306k reference decisions)."""
     torch.manual_seed(11)
     H, S, Np, K = 32, 10, 1024, 50
     model, prior = p_m71_model(H), p_m71_prior(H, S, S, counts_rate=0.003125)

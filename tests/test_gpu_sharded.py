@@ -194,8 +194,10 @@ def test_c3_two_process_gloo_full_size(tmp_path):
 
 
 def test_c3_shape_grid_of_32x32_tiles():
-    """A 4x4 grid of 32x32 tiles (the C3 geometry at reduced N) through one
-    SMCsampler with the reference's lockstep stop: every tile reaches
+    """(Property checks only; the full-size C3 run is
+    test_c3_full_size_lockstep.)  A 4x4 grid of 32x32 tiles (the C3 geometry
+    at reduced N) through one SMCsampler with the reference's lockstep stop:
+    every tile reaches
     temperature 1, log Z and ESS are finite, non-final ESS = rho*N, and each
     tile's result is independent of its neighbours (equal to the same tile
     sampled alone, independent stopping)."""
