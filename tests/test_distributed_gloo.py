@@ -54,6 +54,8 @@ def _worker(rank, world, port, num_tiles, tps, q):
             "locs": tiles[:, None, None, None].repeat(1, 5, 3, 2) + 0.5,    # [T, N, S, 2]
             "log_normalizing_constant": -tiles,                            # [T]
             "pruned_counts": tiles[:, None].repeat(1, 5).to(torch.int64),  # int field
+            # int64 beyond float32's 2^24: gathered in its own dtype, exact
+            "big": tiles.to(torch.int64) + (1 << 40),
         }
         out = gather_tile_results(local, num_tiles, tps, rank, world, dst=0)
         if rank == 0:
@@ -131,6 +133,8 @@ def test_gather_and_lockstep_gloo(world):
     assert torch.equal(full["locs"][..., 0, 0, 0], idx + 0.5)
     assert torch.equal(full["log_normalizing_constant"], -idx)
     assert full["pruned_counts"].dtype == torch.int64
+    assert full["big"].dtype == torch.int64
+    assert torch.equal(full["big"], idx.to(torch.int64) + (1 << 40))
     assert all(k[2] is True for k in keeps)  # rank 1 (and 2) still below 1
 
 
