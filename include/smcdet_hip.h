@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 16
+#define SMCDET_ABI_VERSION 15
 
 /* status codes */
 #define SMCDET_OK 0
@@ -121,18 +121,6 @@ typedef struct smcdet_mh {
   float fluxes_min, fluxes_max;
   float locs_min_h, locs_min_w; /* = Prior.loc_prior.low  (sampler.py:36) */
   float locs_max_h, locs_max_w; /* = Prior.loc_prior.high (sampler.py:37) */
-  /* (ABI 16, nullable; smcdet_mh_sweep / _step only, ignored elsewhere) PSF
-   * window cache: a device workspace of smcdet_mh_psf_cache_floats(...)
-   * floats.  The incremental M71 sweep then keeps, per particle, each
-   * source's (2R+1)^2 PSF window at its current location and loads a moved
-   * source's old PSF from it instead of re-evaluating it (3 exp2 + 1 log2
-   * fewer per window position); the proposal's window is written as it is
-   * evaluated.  The cached values are the ones the sweep would recompute, so
-   * the results are bit-identical with and without it.  Contents need no
-   * initialisation and do not persist between calls (each sweep fills the
-   * windows of its starting state).  Ignored where it does not apply (see
-   * smcdet_mh_psf_cache_floats) and by the fused step's one-launch form. */
-  float* psf_cache;
 } smcdet_mh_t;
 
 /* Optional replay of recorded draws (tests): per MH iteration k, tile t,
@@ -272,14 +260,6 @@ int smcdet_mh_sweep(const smcdet_image_model_t* model,
                     uint32_t flags, float* loglik_out, float* acc_rate,
                     int32_t* acc_count, const int32_t* go,
                     const float* tile_boxes, void* stream);
-
-/* Floats of smcdet_mh_t.psf_cache for a sweep of T tiles x N particles x S
- * sources with this model and these flags: T * N * (S + 1) * ws, ws = (2R+1)^2
- * rounded up to 64, or 0 where the cache does not apply (POISSON model,
- * SMCDET_MH_FULL_RECOMPUTE or SMCDET_MH_SCALAR_SLOTS, tiles of at most 64 or
- * more than 4096 pixels, S > 15).  Negative: invalid arguments. */
-int64_t smcdet_mh_psf_cache_floats(const smcdet_image_model_t* model, int32_t T,
-                                   int32_t N, int32_t S, uint32_t flags);
 
 /* SingleComponentMALA.run (smcdet/kernel.py:133-275), K iterations fused in
  * one launch.  Arguments as smcdet_mh_sweep; mala->locs_stdev and

@@ -23,7 +23,7 @@ SMCDET_RESAMPLE_SYSTEMATIC = 1
 SMCDET_MH_FULL_RECOMPUTE = 1
 SMCDET_MH_COMPONENT_BY_COUNT = 2
 SMCDET_MH_SKIP_DONE = 4
-ABI_VERSION = 16
+ABI_VERSION = 15
 SMCDET_SMC_FREEZE_DONE = 1
 SMCDET_SMC_TWO_LAUNCH = 2
 
@@ -89,8 +89,7 @@ class PriorC(ctypes.Structure):
 class MHC(ctypes.Structure):
     _fields_ = [("num_iters", c_i), ("locs_stdev", c_f), ("fluxes_stdev", c_f),
                 ("fluxes_min", c_f), ("fluxes_max", c_f), ("locs_min_h", c_f),
-                ("locs_min_w", c_f), ("locs_max_h", c_f), ("locs_max_w", c_f),
-                ("psf_cache", c_p)]
+                ("locs_min_w", c_f), ("locs_max_h", c_f), ("locs_max_w", c_f)]
 
 
 class ReplayC(ctypes.Structure):
@@ -133,7 +132,6 @@ _SIGS = {
                               c_p, c_p, c_p, c_p, c_u64, c_u64, c_p, c_u32, c_p, c_p, c_p, c_p,
                               c_p, c_p, c_p], c_i),
     "smcdet_mh_sweep_step_fused": ([c_p, c_i, c_i, c_u32], c_i),
-    "smcdet_mh_psf_cache_floats": ([c_p, c_i, c_i, c_i, c_u32], c_i64),
     "smcdet_mala_sweep": ([c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p,
                            c_p, c_p, c_p, c_u64, c_u64, c_p, c_u32, c_p, c_p, c_p, c_p, c_p],
                           c_i),

@@ -85,8 +85,6 @@ struct MhArgs {
   uint8_t* r_accept;
   // fused SMC iteration: the tile's last workgroup runs temper -> reweight ->
   // next resampling indices (tile.h) on loglik_out right after the sweep
-  float* wcache;                     // PSF window cache [T,N,S+1,ws] (or null)
-  int ws;                            // window stride (floats, >= (2R+1)^2)
   int has_tail;
   TileArgs tail;
 };
@@ -148,77 +146,27 @@ __device__ __forceinline__ void propose_lane(float mu, float c_ph, float c_lZ, f
   }
 }
 
-// PSF window cache (WC, SMCDET_MH_PSF_CACHE): per particle S + 1 windows of
-// (2R+1)^2 raw PSF values (psf_raw at the window's pixels, row-major from the
-// floor anchor minus R), one per source at its current location plus a
-// staging window.  A position's old PSF is loaded from the moved source's
-// window instead of being re-evaluated (3 exp2 + 1 log2 fewer per position);
-// the proposal's new PSF is stored into the staging window as it is
-// evaluated, and an accepted move swaps the two (a 4-bit slot map in SGPRs),
-// so the cache holds exactly the values the kernel would recompute.
-// Out-of-window positions get the offset kOob: the buffer's range check
-// returns 0 for such loads and drops such stores.
-// Addressing: a union-window position (aa, bb) has window index
-// (aa - a_h) * D + (bb - a_w) = c + aa * D + bb for the window's anchors
-// (a_h, a_w) relative to the union box, c = -(a_h * D + a_w) >= 0; each
-// descriptor's base is moved by c and its range cut to ws - c, so one byte
-// offset voff = 4 (q + aa (D - bw)) (q = aa * bw + bb) serves both windows,
-// and the range check of the moved descriptor is the window's own.
-struct WinIO {
-  __amdgpu_buffer_rsrc_t cur;  // the moved source's window at its current location
-  __amdgpu_buffer_rsrc_t stg;  // staging window (receives the proposal's PSF)
-  unsigned dd4;                // 4 (D - bw)
-};
-constexpr int kOob = 0x7ffffff0;
-// a wave-uniform pointer the compiler cannot prove uniform (derived from
-// threadIdx.x >> 6), as SGPRs: buffer descriptors in VGPRs become waterfall loops
-__device__ __forceinline__ float* uniform_ptr(float* p) {
-  const uint64_t v = (uint64_t)(uintptr_t)p;
-  return (float*)(uintptr_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32))
-                              << 32) |
-                             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v));
-}
-__device__ __forceinline__ float wc_load(const __amdgpu_buffer_rsrc_t& r, int off) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
-}
-__device__ __forceinline__ void wc_store(float v, const __amdgpu_buffer_rsrc_t& r, int off) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
-}
-
 // One position of the union window: rate change dl and log-likelihood change.
 // WINDOWS = false when old and new windows coincide (same floor anchors): every
 // position of the (clipped) box is in both.
 // GL: the tile image lives in global memory (tiles above the LDS budget): a
 // masked lane's dummy position HW + lane reads the last pixel instead
-template <int MODEL, bool WINDOWS, bool GL = false, bool WC = false>
+template <int MODEL, bool WINDOWS, bool GL = false>
 __device__ __forceinline__ float position_delta(const DevModel& m, const float* xs,
                                                 const float* lg, const float* lam, int p,
                                                 int aa, int bb, int ph, int pw,
                                                 const Proposal& P, float amp_o, float amp_n,
                                                 int ao_h, int ao_w, int an_h, int an_w,
-                                                float& lnew, const WinIO& wio, int voff) {
+                                                float& lnew) {
   const float fph = (float)ph + 0.5f, fpw = (float)pw + 0.5f;
+  const float dho = fph - P.h, dwo = fpw - P.w;
   const float dhn = fph - P.hn, dwn = fpw - P.wn;
-  const unsigned span = 2u * (unsigned)m.R;
-  float psi_o, psi_n = psf_raw<MODEL>(m, fmaf(dhn, dhn, dwn * dwn));
-  if constexpr (WC) {
-    int vo = voff, vn = voff;
-    if (WINDOWS) {
-      const bool in_o = (unsigned)(aa - ao_h) <= span && (unsigned)(bb - ao_w) <= span;
-      const bool in_n = (unsigned)(aa - an_h) <= span && (unsigned)(bb - an_w) <= span;
-      vo = in_o ? vo : kOob;
-      vn = in_n ? vn : kOob;
-      psi_n = in_n ? psi_n : 0.f;
-    }
-    psi_o = wc_load(wio.cur, vo);
-    wc_store(psi_n, wio.stg, vn);
-  } else {
-    const float dho = fph - P.h, dwo = fpw - P.w;
-    psi_o = psf_raw<MODEL>(m, fmaf(dho, dho, dwo * dwo));
-    if (WINDOWS) {
-      psi_o = ((unsigned)(aa - ao_h) <= span && (unsigned)(bb - ao_w) <= span) ? psi_o : 0.f;
-      psi_n = ((unsigned)(aa - an_h) <= span && (unsigned)(bb - an_w) <= span) ? psi_n : 0.f;
-    }
+  float psi_o = psf_raw<MODEL>(m, fmaf(dho, dho, dwo * dwo));
+  float psi_n = psf_raw<MODEL>(m, fmaf(dhn, dhn, dwn * dwn));
+  if (WINDOWS) {
+    const unsigned span = 2u * (unsigned)m.R;
+    psi_o = ((unsigned)(aa - ao_h) <= span && (unsigned)(bb - ao_w) <= span) ? psi_o : 0.f;
+    psi_n = ((unsigned)(aa - an_h) <= span && (unsigned)(bb - an_w) <= span) ? psi_n : 0.f;
   }
   const float dl = fmaf(amp_n, psi_n, -amp_o * psi_o);
   const float lo = lam[p];
@@ -232,41 +180,24 @@ __device__ __forceinline__ float position_delta(const DevModel& m, const float* 
 // arithmetic runs as packed v_pk_{fma,mul,add}_f32 (one issue for both
 // halves), the transcendentals per half.  Same per-element operation order as
 // position_delta.
-template <int MODEL, bool WINDOWS, bool GL = false, bool WC = false>
+template <int MODEL, bool WINDOWS, bool GL = false>
 __device__ __forceinline__ f2 position_delta2(const DevModel& m, const float* xs, const float* lg,
                                              const float* lam, const int (&p)[2],
                                              const int (&aa)[2], const int (&bb)[2], f2 fph,
                                              f2 fpw, const Proposal& P, float amp_o, float amp_n,
-                                             int ao_h, int ao_w, int an_h, int an_w, f2& lnew,
-                                             const WinIO& wio, const int (&voff)[2]) {
+                                             int ao_h, int ao_w, int an_h, int an_w, f2& lnew) {
+  const f2 dho = fph - P.h, dwo = fpw - P.w;
   const f2 dhn = fph - P.hn, dwn = fpw - P.wn;
-  const unsigned span = 2u * (unsigned)m.R;
-  f2 psi_o, psi_n = psf_raw2<MODEL>(m, fma2(dhn, dhn, dwn * dwn));
-  if constexpr (WC) {
+  f2 psi_o = psf_raw2<MODEL>(m, fma2(dho, dho, dwo * dwo));
+  f2 psi_n = psf_raw2<MODEL>(m, fma2(dhn, dhn, dwn * dwn));
+  if (WINDOWS) {
+    const unsigned span = 2u * (unsigned)m.R;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      int vo = voff[h], vn = voff[h];
-      if (WINDOWS) {
-        const bool in_o = (unsigned)(aa[h] - ao_h) <= span && (unsigned)(bb[h] - ao_w) <= span;
-        const bool in_n = (unsigned)(aa[h] - an_h) <= span && (unsigned)(bb[h] - an_w) <= span;
-        vo = in_o ? vo : kOob;
-        vn = in_n ? vn : kOob;
-        psi_n[h] = in_n ? psi_n[h] : 0.f;
-      }
-      psi_o[h] = wc_load(wio.cur, vo);
-      wc_store(psi_n[h], wio.stg, vn);
-    }
-  } else {
-    const f2 dho = fph - P.h, dwo = fpw - P.w;
-    psi_o = psf_raw2<MODEL>(m, fma2(dho, dho, dwo * dwo));
-    if (WINDOWS) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        psi_o[h] =
-            ((unsigned)(aa[h] - ao_h) <= span && (unsigned)(bb[h] - ao_w) <= span) ? psi_o[h] : 0.f;
-        psi_n[h] =
-            ((unsigned)(aa[h] - an_h) <= span && (unsigned)(bb[h] - an_w) <= span) ? psi_n[h] : 0.f;
-      }
+      psi_o[h] = ((unsigned)(aa[h] - ao_h) <= span && (unsigned)(bb[h] - ao_w) <= span) ? psi_o[h]
+                                                                                       : 0.f;
+      psi_n[h] = ((unsigned)(aa[h] - an_h) <= span && (unsigned)(bb[h] - an_w) <= span) ? psi_n[h]
+                                                                                       : 0.f;
     }
   }
   const f2 dl = fma2(psi_n, amp_n, -amp_o * psi_o);
@@ -310,12 +241,8 @@ constexpr int mh_slots() { return PPL == 1 ? 1 : kSlots; }
 // global memory (L2-resident) and the particle's rate image lives in rate_out
 // (row stride H*W + 64: the 64 dummy cells of masked lanes), which the sweep
 // updates in place; LDS holds only the workgroup counters.
-// WC: the PSF window cache (a.wcache; WinIO above): M71, incremental,
-// paired, LDS tiles of more than 64 pixels, S <= 15 (host-checked).
-template <int MODEL, bool REPLAY, bool FULL, int PPL, bool PAIRED, bool TAIL, bool GL = false,
-          bool WC = false>
+template <int MODEL, bool REPLAY, bool FULL, int PPL, bool PAIRED, bool TAIL, bool GL = false>
 __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_kernel(MhArgs a) {
-  static_assert(!WC || (!FULL && !GL && PAIRED && PPL != 1), "window cache: unsupported variant");
   constexpr int NSL = mh_slots<PPL>();
   extern __shared__ float smem[];
   __shared__ int wg_acc, wg_done;  // last-iteration accepts / finished waves of this workgroup
@@ -421,31 +348,6 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     cur_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
   }
   lam[HW + lane] = m.bg;
-  // PSF window cache: source s's window at its current location in slot s,
-  // slot S free for staging (psf_raw at the same arguments as position_delta)
-  [[maybe_unused]] float* wcb = nullptr;
-  [[maybe_unused]] uint64_t wmap = 0;
-  [[maybe_unused]] int wfree = 0;
-  if constexpr (WC) {
-    // (pid is wave-uniform, but derives from threadIdx.x: made an SGPR here so
-    // the buffer descriptors stay scalar -- no waterfall loops)
-    wcb = uniform_ptr(a.wcache + pid * (size_t)(S + 1) * a.ws);
-    const int D = 2 * m.R + 1, DD = D * D;
-    const float inv_d = 1.0f / (float)D;
-    for (int s = 0; s < S; ++s) {
-      const float h = readlane(sh, s), w = readlane(sw, s);
-      const int oh = ifloor16(h) - m.R, ow = ifloor16(w) - m.R;
-      float* dst = wcb + s * a.ws;
-      for (int q = lane; q < DD; q += kWave) {
-        const int i = (int)(((float)q + 0.5f) * inv_d);
-        const int jj = q - i * D;
-        const float dho = ((float)(oh + i) + 0.5f) - h, dwo = ((float)(ow + jj) + 0.5f) - w;
-        dst[q] = psf_raw<MODEL>(m, fmaf(dho, dho, dwo * dwo));
-      }
-      wmap |= (uint64_t)s << (4 * s);
-    }
-    wfree = S;
-  }
   SMC_TRACE(trow, 3);
 
   // ---- proposals, batched: lane 3b+d proposes dimension d (h, w, flux) of
@@ -643,18 +545,6 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
       const bool same = (fh0 == fh1) && (fw0 == fw1);
       const int ao_h = fh0 - m.R - r0, ao_w = fw0 - m.R - c0;
       const int an_h = fh1 - m.R - r0, an_w = fw1 - m.R - c0;
-      WinIO wio;
-      wio.dd4 = 0;
-      if constexpr (WC) {
-        const int D = 2 * m.R + 1;
-        const int cs = (int)((wmap >> (4 * P.j)) & 15u);
-        const int co = -(ao_h * D + ao_w), cn = -(an_h * D + an_w);
-        wio.cur = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(wcb + cs * a.ws + co), (short)0,
-                                                    4 * (a.ws - co), 0x00020000);
-        wio.stg = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(wcb + wfree * a.ws + cn), (short)0,
-                                                    4 * (a.ws - cn), 0x00020000);
-        wio.dd4 = 4u * (unsigned)(D - bw);
-      }
       // NS predicated slots in one basic block, with the (independent) next
       // proposal in the same block so the scheduler can interleave the two
       auto slots = [&](auto NS, auto WIN) -> float {
@@ -670,9 +560,8 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           const int ph = r0 + aa, pw = c0 + bb;
           const int p = valid ? (int)__umul24((unsigned)ph, (unsigned)m.W) + pw : HW + lane;
           float lnew;
-          const int voff = (int)__umul24((unsigned)aa, wio.dd4) + 4 * q;
-          const float e = position_delta<MODEL, win, GL, WC>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
-                                                     amp_n, ao_h, ao_w, an_h, an_w, lnew, wio, voff);
+          const float e = position_delta<MODEL, win, GL>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
+                                                     amp_n, ao_h, ao_w, an_h, an_w, lnew);
           acc += valid ? e : 0.f;
           s_lam[i] = lnew;
           s_pix[i] = p;
@@ -688,7 +577,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
         f2 acc = {0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < np; ++i) {
-          int aa[2], bb[2], p[2], voff[2];
+          int aa[2], bb[2], p[2];
           bool valid[2];
           f2 fph, fpw;
 #pragma unroll
@@ -701,11 +590,10 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
             p[h] = valid[h] ? (int)__umul24((unsigned)ph, (unsigned)m.W) + pw : HW + lane;
             fph[h] = (float)ph + 0.5f;
             fpw[h] = (float)pw + 0.5f;
-            voff[h] = (int)__umul24((unsigned)aa[h], wio.dd4) + 4 * q;
           }
           f2 lnew;
-          f2 e = position_delta2<MODEL, win, GL, WC>(m, xs, lg, lam, p, aa, bb, fph, fpw, P, amp_o, amp_n,
-                                             ao_h, ao_w, an_h, an_w, lnew, wio, voff);
+          f2 e = position_delta2<MODEL, win, GL>(m, xs, lg, lam, p, aa, bb, fph, fpw, P, amp_o, amp_n,
+                                             ao_h, ao_w, an_h, an_w, lnew);
           e.x = valid[0] ? e.x : 0.f;
           e.y = valid[1] ? e.y : 0.f;
           acc += e;
@@ -723,9 +611,8 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           const int ph = r0 + aa, pw = c0 + bb;
           const int p = valid ? (int)__umul24((unsigned)ph, (unsigned)m.W) + pw : HW + lane;
           float lnew;
-          const int voff = (int)__umul24((unsigned)aa, wio.dd4) + 4 * q;
-          const float e = position_delta<MODEL, win, GL, WC>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
-                                                     amp_n, ao_h, ao_w, an_h, an_w, lnew, wio, voff);
+          const float e = position_delta<MODEL, win, GL>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
+                                                     amp_n, ao_h, ao_w, an_h, an_w, lnew);
           acc1 = valid ? e : 0.f;
           s_lam[2 * np] = lnew;
           s_pix[2 * np] = p;
@@ -755,9 +642,8 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           const int ph = r0 + aa, pw = c0 + bb;
           const int p = (int)__umul24((unsigned)ph, (unsigned)m.W) + pw;
           float lnew;
-          const int voff = (int)__umul24((unsigned)aa, wio.dd4) + 4 * q;
-          acc += position_delta<MODEL, true, GL, WC>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o, amp_n,
-                                             ao_h, ao_w, an_h, an_w, lnew, wio, voff);
+          acc += position_delta<MODEL, true, GL>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o, amp_n,
+                                             ao_h, ao_w, an_h, an_w, lnew);
           if constexpr (decltype(WRITE)::value) lam[p] = lnew;
         }
         return acc;
@@ -856,12 +742,6 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           wave_sync();
         }
         cur_ll += (double)dll;
-      }
-      if constexpr (WC) {  // the staging window becomes source j's
-        const unsigned sh4 = 4u * (unsigned)P.j;
-        const int cs = (int)((wmap >> sh4) & 15u);
-        wmap = (wmap & ~(15ull << sh4)) | ((uint64_t)wfree << sh4);
-        wfree = cs;
       }
       // source j takes the proposal (v_writelane)
       sh = writelane(P.hn, P.j, sh);
@@ -981,15 +861,6 @@ static int launch_mh1(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
                             : (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, false, false>;
   int rc = ensure_lds(fn, lds);
   if (rc) return rc;
-  if constexpr (MODEL == SMCDET_MODEL_M71 && kPair && PPL != 1) {
-    if (a.wcache && paired && !tail) {
-      auto wfn = mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, false, false, true>;
-      rc = ensure_lds((const void*)wfn, lds);
-      if (rc) return rc;
-      launch_sweep(wfn, grid, dim3(kMhBlock), lds, st, a);
-      return SMCDET_OK;
-    }
-  }
   if (tail)
     launch_sweep(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, kTail>, grid, dim3(kMhBlock), lds, st, a);
   else if (paired)
@@ -1042,22 +913,6 @@ using namespace smcdet;
 
 SMCDET_TRACE_READER(smcdet_trace_read_mh)
 SMCDET_WAVE_READER(smcdet_trace_read_waves)
-
-// floats per window of the PSF window cache, 0 where it does not apply
-static int psf_cache_stride(const smcdet_image_model_t& m, int S, uint32_t flags) {
-  if (m.model != SMCDET_MODEL_M71 || S < 1 || S > 15) return 0;
-  if (flags & (SMCDET_MH_FULL_RECOMPUTE | SMCDET_MH_SCALAR_SLOTS)) return 0;
-  if (m.H * m.W <= 64 || m.H * m.W > kMaxLdsPixels || m.psf_radius < 0) return 0;
-  const int D = 2 * m.psf_radius + 1;
-  return (D * D + 63) / 64 * 64;
-}
-
-extern "C" int64_t smcdet_mh_psf_cache_floats(const smcdet_image_model_t* model, int32_t T,
-                                              int32_t N, int32_t S, uint32_t flags) {
-  if (!model || T < 0 || N < 0 || S < 0) return -1;
-  const int ws = psf_cache_stride(*model, S, flags);
-  return (int64_t)T * N * (S + 1) * ws;
-}
 
 // the fused step's shape test; lds: the launch's dynamic LDS bytes
 static bool tail_fusable(const smcdet_image_model_t& m, int N, int S, uint32_t flags,
@@ -1207,10 +1062,6 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
     }
   }
   const bool full = (flags & SMCDET_MH_FULL_RECOMPUTE) != 0;
-  if (mh->psf_cache && psf_cache_stride(*model, S, flags) > 0) {
-    a.wcache = mh->psf_cache;
-    a.ws = psf_cache_stride(*model, S, flags);
-  }
   a.ablate = flags & (SMCDET_MH_ABLATE_LIKELIHOOD | SMCDET_MH_ABLATE_PROPOSAL);
   a.by_count = (flags & SMCDET_MH_COMPONENT_BY_COUNT) != 0;
   a.scalar_slots = (flags & SMCDET_MH_SCALAR_SLOTS) != 0;

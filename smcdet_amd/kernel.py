@@ -45,11 +45,7 @@ class SingleComponentMH(object):
         self.rng = None           # PhiloxStream; SMCsampler installs its own
         self.debug_flags = 0      # SMCDET_MH_ABLATE_* timing diagnostics (never for sampling)
         self.last_loglik = None   # log-likelihood of the state returned by run()
-        # PSF window cache (smcdet_mh_t.psf_cache): the sweep loads a moved
-        # source's old PSF window instead of re-evaluating it; same results
-        self.psf_cache = True
         self._acc_ws = {}
-        self._psf_ws = {}
 
     @staticmethod
     def _resolve(log_target, prior, image_model):
@@ -87,25 +83,6 @@ class SingleComponentMH(object):
         if ws is None:
             ws = torch.zeros(2 * T, device=dev, dtype=torch.int32)
             self._acc_ws[key] = ws
-        return ws
-
-    def _psf_workspace(self, cm, T, N, S, flags, dev):
-        """The sweep's PSF window-cache workspace (smcdet_mh_psf_cache_floats
-        floats; no initialisation, nothing persists between calls), kept per
-        size and device; None where the cache does not apply."""
-        if not self.psf_cache or self._entry != "smcdet_mh_sweep":
-            return None
-        n = int(_hip.lib().smcdet_mh_psf_cache_floats(_hip.ref(cm), T, N, S, flags))
-        if n < 0:
-            raise ValueError("smcdet_mh_psf_cache_floats: invalid arguments")
-        if n == 0:
-            return None
-        key = (n, str(dev))
-        ws = self._psf_ws.get(key)
-        if ws is None:
-            self._psf_ws.clear()  # one workspace at a time (the sampler's shape)
-            ws = torch.empty(n, device=dev, dtype=torch.float32)
-            self._psf_ws[key] = ws
         return ws
 
     @staticmethod
@@ -205,8 +182,6 @@ class SingleComponentMH(object):
         if self.component_by_count:
             flags |= _hip.SMCDET_MH_COMPONENT_BY_COUNT
         flags |= int(extra_flags)
-        psf_ws = self._psf_workspace(cm, T, N, S, flags, dev)
-        ch.psf_cache = psf_ws.data_ptr() if psf_ws is not None else None
         extra = []
         if self._entry == "smcdet_mh_sweep":
             if tile_boxes is not None:

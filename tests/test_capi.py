@@ -55,9 +55,7 @@ def test_struct_layouts_match_header():
     # sizes of the POD structs as the header declares them (all 4-byte fields)
     assert ctypes.sizeof(_hip.ImageModelC) == 4 * 4 + 4 * 2 + 6 * 4 + 3 * 4
     assert ctypes.sizeof(_hip.PriorC) == 3 * 4 + 7 * 4
-    # 9 four-byte fields, then the psf_cache pointer (ABI 16) at offset 40
-    assert _hip.MHC.psf_cache.offset == 40
-    assert ctypes.sizeof(_hip.MHC) == 40 + ctypes.sizeof(ctypes.c_void_p)
+    assert ctypes.sizeof(_hip.MHC) == 4 + 8 * 4
     assert ctypes.sizeof(_hip.ReplayC) == 6 * ctypes.sizeof(ctypes.c_void_p)
 
 
@@ -110,27 +108,3 @@ def test_launch_timing_pool_without_gpu():
     assert L.smcdet_launch_timing(-1) == -1
     assert L.smcdet_launch_timing(0) == 0
     assert _hip.launch_timing_read(4) == []
-
-
-def test_psf_cache_floats():
-    """smcdet_mh_psf_cache_floats: T*N*(S+1)*ws (ws = (2R+1)^2 rounded up to
-    64) for the incremental M71 sweep on LDS tiles of 65..4096 pixels with
-    S <= 15; 0 where the cache does not apply; -1 for invalid arguments."""
-    L = _hip.lib()
-    m = _hip.ImageModelC()
-    m.model, m.H, m.W, m.psf_radius = 1, 32, 32, 8
-    assert L.smcdet_mh_psf_cache_floats(ctypes.byref(m), 2, 4096, 10, 0) == 2 * 4096 * 11 * 320
-    m.psf_radius = 3  # 7x7 = 49 -> 64
-    assert L.smcdet_mh_psf_cache_floats(ctypes.byref(m), 1, 8, 15, 0) == 8 * 16 * 64
-    assert L.smcdet_mh_psf_cache_floats(ctypes.byref(m), 1, 8, 16, 0) == 0
-    assert L.smcdet_mh_psf_cache_floats(ctypes.byref(m), 1, 8, 10,
-                                        _hip.SMCDET_MH_FULL_RECOMPUTE) == 0
-    assert L.smcdet_mh_psf_cache_floats(ctypes.byref(m), 1, 8, 10, 1024) == 0  # scalar slots
-    m.H = m.W = 8  # the small-tile instantiation
-    assert L.smcdet_mh_psf_cache_floats(ctypes.byref(m), 1, 8, 10, 0) == 0
-    m.H = m.W = 128  # global-memory sweep
-    assert L.smcdet_mh_psf_cache_floats(ctypes.byref(m), 1, 8, 10, 0) == 0
-    m.H = m.W = 32
-    m.model = 2  # Poisson model
-    assert L.smcdet_mh_psf_cache_floats(ctypes.byref(m), 1, 8, 10, 0) == 0
-    assert L.smcdet_mh_psf_cache_floats(None, 1, 8, 10, 0) == -1
