@@ -525,7 +525,8 @@ def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
 def vs_reference(dev, which="c2_moderate", n_runs=128):
     """North-star parity at the headline geometry, outside the timed region:
     the reference's recorded runs (tests/golden/stats_<which>.json: one 32x32
-    M71 tile, S=10, N=4096 or 512, K=20, systematic, >= 20 seeds) against n_runs runs
+    M71 tile, S=10, N=4096 at K=100 (8 seeds) or K=20 (20 seeds), or N=512,
+    K=20 (32 seeds), systematic) against n_runs runs
     of this sampler on the same image -- one launch grid of n_runs independent
     copies of the tile (independent stopping = one single-tile run per copy,
     each with its own Philox streams).  Means and standard errors of log Z,
@@ -865,9 +866,11 @@ def main():
                                      "ms_per_iteration": run_s / max(int(s2.iter), 1) * 1e3,
                                      "temperature_min": float(s2.temperature.min())}
     if rank == 0 and args.workload == "c2" and args.kernel == "mh" and not args.no_vs_ref:
-        # the headline particle count first (N = 4096, tests/golden/
-        # stats_c2_moderate_4096.json), then the reduced-N target
-        for key, which in (("vs_reference", "c2_moderate_4096"),
+        # the headline configuration first (N = 4096, K = 100: tests/golden/
+        # stats_c2_moderate_4096_k100.json), then N = 4096 at K = 20 (more
+        # reference seeds) and the reduced-N target
+        for key, which in (("vs_reference", "c2_moderate_4096_k100"),
+                           ("vs_reference_k20", "c2_moderate_4096"),
                            ("vs_reference_n512", "c2_moderate")):
             try:
                 r = vs_reference(dev, which)
