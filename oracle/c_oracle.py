@@ -46,6 +46,7 @@ def lib():
         _lib = ctypes.CDLL(LIB)
         _lib.mh_oracle_sweep.restype = ctypes.c_int
         _lib.mala_oracle_sweep.restype = ctypes.c_int
+        _lib.mh_oracle_loglik.restype = ctypes.c_int
     return _lib
 
 
@@ -105,6 +106,22 @@ def mh_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mh, replay=No
     acc = acc.reshape(nH, nW, N)
     rate = (acc == 1).mean(-1)
     return (l, f, rate, acc == 2) if frozen_out else (l, f, rate)
+
+
+def loglik(tiled_image, locs, fluxes, model, threads=0):
+    """Image log-likelihoods [nH,nW,N] (float64) of the catalogs, by the C
+    restatement (images.py:159-175 / :85-102)."""
+    img = np.ascontiguousarray(tiled_image, dtype=np.float32)
+    nH, nW, N, S, _ = np.shape(locs)
+    l = np.ascontiguousarray(locs, dtype=np.float32)
+    f = np.ascontiguousarray(fluxes, dtype=np.float32)
+    out = np.empty(nH * nW * N, np.float64)
+    prior = O.M71PriorP(S, S, 0.0, model.H, model.W, 0, 1.0, 1.0, 2.0) \
+        if isinstance(model, O.M71Model) else O.ParetoPriorP(S, S, model.H, model.W, 0, 1.0, 1.0)
+    m, _, _ = _pack(model, prior, O.MHParams(0, 1.0, 1.0, 0.1, 1.0))
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    lib().mh_oracle_loglik(ctypes.byref(m), P(img), P(l), P(f), nH * nW, N, S, threads, P(out))
+    return out.reshape(nH, nW, N)
 
 
 def mala_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mala, replay=None, seed=0,

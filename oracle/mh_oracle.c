@@ -188,6 +188,41 @@ static uint64_t splitmix(uint64_t* s) {
 static double urand(uint64_t* s) { return (double)(splitmix(s) >> 40) * (1.0 / 16777216.0); }
 
 /*
+ * Image log-likelihood of T*N particles (images.py:159-175 / :85-102), float64
+ * accumulation as loglik() above: out[T*N].  For the oracle SMC runs
+ * (tests/golden/make_oracle_stats.py).  Returns 0.
+ */
+int mh_oracle_loglik(const om_model_t* m, const float* image, const float* locs,
+                     const float* fluxes, int T, int N, int S, int threads, double* out) {
+  const int HW = m->H * m->W;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#endif
+#pragma omp parallel
+  {
+    double* h = malloc(sizeof(double) * S * 3);
+    double* w = h + S;
+    double* f = w + S;
+    double* rate = malloc(sizeof(double) * HW * 2);
+    double* lgx = rate + HW;
+#pragma omp for schedule(static)
+    for (long pid = 0; pid < (long)T * N; ++pid) {
+      const float* x = image + (size_t)(pid / N) * HW;
+      for (int p = 0; p < HW; ++p) lgx[p] = lgamma((double)x[p] + 1.0);
+      for (int s = 0; s < S; ++s) {
+        h[s] = locs[(pid * S + s) * 2 + 0];
+        w[s] = locs[(pid * S + s) * 2 + 1];
+        f[s] = fluxes[pid * S + s];
+      }
+      out[pid] = loglik(m, x, h, w, f, S, rate, lgx);
+    }
+    free(h);
+    free(rate);
+  }
+  return 0;
+}
+
+/*
  * One MH sweep over T*N particles.  image [T,H,W], counts [T,N], locs
  * [T,N,S,2] and fluxes [T,N,S] updated in place; tau [T].  Draws come from
  * the replay arrays (comp [K,T,N], uloc [K,T,N,2], uflux/uacc [K,T,N]) when
