@@ -112,6 +112,8 @@ def parse():
     ap.add_argument("--no-c3", action="store_true")
     # skip the untimed step-spread passes
     ap.add_argument("--no-spread", action="store_true")
+    # diagnostic MH flags (A/B timing: e.g. 2048 = SMCDET_MH_NO_PSF_CACHE)
+    ap.add_argument("--mh-debug-flags", type=int, default=0)
     return ap.parse_args()
 
 
@@ -120,8 +122,10 @@ def mutation_kernel(args, K, full_recompute=False):
     p = M71
     if args.kernel == "mala":
         return SingleComponentMALA(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"])
-    return SingleComponentMH(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"],
-                             full_recompute=full_recompute)
+    mh = SingleComponentMH(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"],
+                           full_recompute=full_recompute)
+    mh.debug_flags = args.mh_debug_flags
+    return mh
 
 
 def make_models(H, S):

@@ -86,6 +86,9 @@ extern "C" {
 /* diagnostic: evaluate the union window one position per lane instead of two
  * (packed arithmetic); same results up to float32 summation order */
 #define SMCDET_MH_SCALAR_SLOTS 1024u
+/* diagnostic: small tiles (H*W <= 64) without the per-wave PSF cache (the
+ * moved source's old PSF re-evaluated each iteration); same results */
+#define SMCDET_MH_NO_PSF_CACHE 2048u
 
 /* Image model (smcdet/images.py:6-26 ImageModel, :105-145 M71ImageModel). */
 typedef struct smcdet_image_model {

@@ -61,6 +61,7 @@ struct MhArgs {
   int by_count;                      // SMCDET_MH_COMPONENT_BY_COUNT
   int scalar_slots;                  // SMCDET_MH_SCALAR_SLOTS (diagnostic)
   int skip_done;                     // SMCDET_MH_SKIP_DONE
+  int no_psf_cache;                  // SMCDET_MH_NO_PSF_CACHE (diagnostic)
   const float* img;                  // [T,H,W]
   const float* temperature;          // [T]
   const int64_t* ancestors;          // [T,N] or null
@@ -215,6 +216,36 @@ __device__ __forceinline__ f2 position_delta2(const DevModel& m, const float* xs
   return pix_delta2<MODEL>(m, x, lgx, lo, dl);
 }
 
+// Small tiles with the PSF cache (PC): the moved source's old PSF values come
+// from the wave's cache row of that source (its raw PSF at every tile pixel,
+// 0 outside its window) instead of being re-evaluated; the new window's
+// values are returned for the cache update on accept.  Both are the values
+// position_delta computes, by the same operations on the same inputs (the
+// cached row was evaluated at the source's current position), so decisions
+// and rates are bit-identical to the uncached sweep.
+template <int MODEL, bool WINDOWS>
+__device__ __forceinline__ float position_delta_pc(const DevModel& m, const float* xs,
+                                                   const float* lg, const float* lam,
+                                                   const float* pcj, int p, bool valid, int aa,
+                                                   int bb, int ph, int pw, const Proposal& P,
+                                                   float amp_o, float amp_n, int an_h, int an_w,
+                                                   float& lnew, float& psi_new) {
+  const float fph = (float)ph + 0.5f, fpw = (float)pw + 0.5f;
+  const float dhn = fph - P.hn, dwn = fpw - P.wn;
+  const float psi_o = pcj[valid ? p : 0];  // (a masked lane's value is discarded)
+  float psi_n = psf_raw<MODEL>(m, fmaf(dhn, dhn, dwn * dwn));
+  if (WINDOWS) {
+    const unsigned span = 2u * (unsigned)m.R;
+    psi_n = ((unsigned)(aa - an_h) <= span && (unsigned)(bb - an_w) <= span) ? psi_n : 0.f;
+  }
+  psi_new = psi_n;
+  const float dl = fmaf(amp_n, psi_n, -amp_o * psi_o);
+  const float lo = lam[p];
+  lnew = lo + dl;
+  const float lgx = (MODEL == SMCDET_MODEL_POISSON) ? lg[p] : 0.0f;
+  return pix_delta<MODEL>(m, xs[p], lgx, lo, dl);
+}
+
 // PPL > 0: tiles of <= 64*PPL pixels rendered in registers (render_regs);
 // PPL = 0: LDS render (larger tiles)
 // PAIRED: union-window positions two per lane in packed arithmetic (default);
@@ -241,8 +272,12 @@ constexpr int mh_slots() { return PPL == 1 ? 1 : kSlots; }
 // global memory (L2-resident) and the particle's rate image lives in rate_out
 // (row stride H*W + 64: the 64 dummy cells of masked lanes), which the sweep
 // updates in place; LDS holds only the workgroup counters.
-template <int MODEL, bool REPLAY, bool FULL, int PPL, bool PAIRED, bool TAIL, bool GL = false>
+// PC: small tiles (PPL == 1, incremental) with the per-wave PSF cache in LDS
+// (S rows of H*W floats after the rate images; position_delta_pc).
+template <int MODEL, bool REPLAY, bool FULL, int PPL, bool PAIRED, bool TAIL, bool GL = false,
+          bool PC = false>
 __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_kernel(MhArgs a) {
+  static_assert(!PC || (PPL == 1 && !FULL && !GL && !TAIL), "PSF cache: small incremental tiles");
   constexpr int NSL = mh_slots<PPL>();
   extern __shared__ float smem[];
   __shared__ int wg_acc, wg_done;  // last-iteration accepts / finished waves of this workgroup
@@ -348,6 +383,22 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     cur_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
   }
   lam[HW + lane] = m.bg;
+  // the PSF cache: row s = source s's raw PSF at every pixel, 0 outside its
+  // (2R+1)^2 window anchored at floor(loc) -- position_delta's old-window value
+  [[maybe_unused]] float* pcw = nullptr;
+  if constexpr (PC) {
+    pcw = smem + (kImg + kMhWaves) * HWp + wave * S * HW;
+    const int ph = lane / m.W, pw = lane - ph * m.W;
+    const float fph = (float)ph + 0.5f, fpw = (float)pw + 0.5f;
+    for (int s = 0; s < S; ++s) {
+      const float hs = readlane(sh, s), ws = readlane(sw, s);
+      const int fh = ifloor16(hs), fw = ifloor16(ws);
+      const float dh = fph - hs, dw = fpw - ws;
+      const float v = psf_raw<MODEL>(m, fmaf(dh, dh, dw * dw));
+      if (lane < HW) pcw[s * HW + lane] = (abs(ph - fh) <= m.R && abs(pw - fw) <= m.R) ? v : 0.f;
+    }
+    wave_sync();
+  }
   SMC_TRACE(trow, 3);
 
   // ---- proposals, batched: lane 3b+d proposes dimension d (h, w, flux) of
@@ -514,6 +565,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     double new_ll = 0.0;
     float s_lam[NSL];
     int s_pix[NSL];
+    [[maybe_unused]] float s_psi = 0.f;  // PC: the new window's PSF values (one slot)
     int npos = 0, bw = 1, r0 = 0, c0 = 0, nslots = 0;
     if constexpr (FULL) {
       const float ch = lane == P.j ? P.hn : sh, cw = lane == P.j ? P.wn : sw;
@@ -559,9 +611,13 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           const int bb = q - (int)__umul24((unsigned)aa, (unsigned)bw);
           const int ph = r0 + aa, pw = c0 + bb;
           const int p = valid ? (int)__umul24((unsigned)ph, (unsigned)m.W) + pw : HW + lane;
-          float lnew;
-          const float e = position_delta<MODEL, win, GL>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
-                                                     amp_n, ao_h, ao_w, an_h, an_w, lnew);
+          float lnew, e;
+          if constexpr (PC)
+            e = position_delta_pc<MODEL, win>(m, xs, lg, lam, pcw + P.j * HW, p, valid, aa, bb, ph,
+                                              pw, P, amp_o, amp_n, an_h, an_w, lnew, s_psi);
+          else
+            e = position_delta<MODEL, win, GL>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o, amp_n,
+                                               ao_h, ao_w, an_h, an_w, lnew);
           acc += valid ? e : 0.f;
           s_lam[i] = lnew;
           s_pix[i] = p;
@@ -738,7 +794,11 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
         cur_ll = new_ll;
       } else {
         if constexpr (NSL == 1) {
-          if (nslots == 1) lam[s_pix[0]] = s_lam[0];
+          if (nslots == 1) {
+            lam[s_pix[0]] = s_lam[0];
+            if constexpr (PC)  // (masked lanes: s_pix = HW + lane, outside the row)
+              if (s_pix[0] < HW) pcw[P.j * HW + s_pix[0]] = s_psi;
+          }
           wave_sync();
         }
         cur_ll += (double)dll;
@@ -856,7 +916,20 @@ static int launch_mh1(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
   constexpr bool kTail = !FULL && PPL != 1;
   const bool tail = kTail && paired && a.has_tail;
   if (a.has_tail && !tail) return set_error(SMCDET_EINVAL, "fused step: unsupported shape");
-  const void* fn = tail     ? (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, kTail>
+  if constexpr (PPL == 1 && !FULL) {
+    // small tiles: the PSF cache (S rows of H*W floats per wave) where the
+    // SMCDET_SMALL_TILE_WAVES workgroups per CU still fit the 160 KiB LDS
+    const size_t lds_pc = lds + (size_t)kMhWaves * a.S * a.m.H * a.m.W * sizeof(float);
+    if (paired && !a.no_psf_cache &&
+        (size_t)SMCDET_SMALL_TILE_WAVES * (lds_pc + 1024) <= 160 * 1024) {
+      auto kpc = mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, true>;
+      int rc = ensure_lds((const void*)kpc, lds_pc);
+      if (rc) return rc;
+      launch_sweep(kpc, grid, dim3(kMhBlock), lds_pc, st, a);
+      return SMCDET_OK;
+    }
+  }
+  const void* fn = tail     ?(const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, kTail>
                    : paired ? (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, false>
                             : (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, false, false>;
   int rc = ensure_lds(fn, lds);
@@ -1066,6 +1139,7 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
   a.by_count = (flags & SMCDET_MH_COMPONENT_BY_COUNT) != 0;
   a.scalar_slots = (flags & SMCDET_MH_SCALAR_SLOTS) != 0;
   a.skip_done = (flags & SMCDET_MH_SKIP_DONE) != 0;
+  a.no_psf_cache = (flags & SMCDET_MH_NO_PSF_CACHE) != 0;
   rc = a.m.model == SMCDET_MODEL_M71
            ? launch_mh<SMCDET_MODEL_M71>(a, replay != nullptr, full, grid, lds, st)
            : launch_mh<SMCDET_MODEL_POISSON>(a, replay != nullptr, full, grid, lds, st);
