@@ -89,6 +89,9 @@ extern "C" {
 /* diagnostic: small tiles (H*W <= 64) without the per-wave PSF cache (the
  * moved source's old PSF re-evaluated each iteration); same results */
 #define SMCDET_MH_NO_PSF_CACHE 2048u
+/* diagnostic: M71 tiles of 65..1024 pixels without the per-wave 1/v image
+ * (each pixel's 1/(s0^2 + eta*rate) formed per use); same results */
+#define SMCDET_MH_NO_RCP_CACHE 4096u
 
 /* Image model (smcdet/images.py:6-26 ImageModel, :105-145 M71ImageModel). */
 typedef struct smcdet_image_model {

@@ -62,6 +62,7 @@ struct MhArgs {
   int scalar_slots;                  // SMCDET_MH_SCALAR_SLOTS (diagnostic)
   int skip_done;                     // SMCDET_MH_SKIP_DONE
   int no_psf_cache;                  // SMCDET_MH_NO_PSF_CACHE (diagnostic)
+  int no_rcp_cache;                  // SMCDET_MH_NO_RCP_CACHE (diagnostic)
   const float* img;                  // [T,H,W]
   const float* temperature;          // [T]
   const int64_t* ancestors;          // [T,N] or null
@@ -152,13 +153,14 @@ __device__ __forceinline__ void propose_lane(float mu, float c_ph, float c_lZ, f
 // position of the (clipped) box is in both.
 // GL: the tile image lives in global memory (tiles above the LDS budget): a
 // masked lane's dummy position HW + lane reads the last pixel instead
-template <int MODEL, bool WINDOWS, bool GL = false>
+template <int MODEL, bool WINDOWS, bool GL = false, bool RV = false>
 __device__ __forceinline__ float position_delta(const DevModel& m, const float* xs,
-                                                const float* lg, const float* lam, int p,
+                                                const float* lg, const float* lam,
+                                                const float* rv, int p,
                                                 int aa, int bb, int ph, int pw,
                                                 const Proposal& P, float amp_o, float amp_n,
                                                 int ao_h, int ao_w, int an_h, int an_w,
-                                                float& lnew) {
+                                                float& lnew, float& rnew) {
   const float fph = (float)ph + 0.5f, fpw = (float)pw + 0.5f;
   const float dho = fph - P.h, dwo = fpw - P.w;
   const float dhn = fph - P.hn, dwn = fpw - P.wn;
@@ -174,6 +176,16 @@ __device__ __forceinline__ float position_delta(const DevModel& m, const float* 
   lnew = lo + dl;
   const float lgx = (MODEL == SMCDET_MODEL_POISSON) ? lg[p] : 0.0f;
   const float x = GL ? xs[min(p, m.H * m.W - 1)] : xs[p];
+  if constexpr (RV) {
+    // M71 with the 1/v cache: pix_delta's operations, r0 read, v0 not formed
+    const float r0 = rv[p];
+    const float v1 = fmaf(m.eta, lnew, m.s0sq);
+    const float r1 = fast_rcp(v1);
+    rnew = r1;
+    const float d0 = x - lo, d1 = x - lnew;
+    const float t = fmaf(d0 * d0, r0, -(d1 * d1) * r1);
+    return fmaf(0.5f, t, (-0.5f * kLn2) * fast_log2(v1 * r0));
+  }
   return pix_delta<MODEL>(m, x, lgx, lo, dl);
 }
 
@@ -181,12 +193,13 @@ __device__ __forceinline__ float position_delta(const DevModel& m, const float* 
 // arithmetic runs as packed v_pk_{fma,mul,add}_f32 (one issue for both
 // halves), the transcendentals per half.  Same per-element operation order as
 // position_delta.
-template <int MODEL, bool WINDOWS, bool GL = false>
+template <int MODEL, bool WINDOWS, bool GL = false, bool RV = false>
 __device__ __forceinline__ f2 position_delta2(const DevModel& m, const float* xs, const float* lg,
-                                             const float* lam, const int (&p)[2],
+                                             const float* lam, const float* rv, const int (&p)[2],
                                              const int (&aa)[2], const int (&bb)[2], f2 fph,
                                              f2 fpw, const Proposal& P, float amp_o, float amp_n,
-                                             int ao_h, int ao_w, int an_h, int an_w, f2& lnew) {
+                                             int ao_h, int ao_w, int an_h, int an_w, f2& lnew,
+                                             f2& rnew) {
   const f2 dho = fph - P.h, dwo = fpw - P.w;
   const f2 dhn = fph - P.hn, dwn = fpw - P.wn;
   f2 psi_o = psf_raw2<MODEL>(m, fma2(dho, dho, dwo * dwo));
@@ -211,6 +224,16 @@ __device__ __forceinline__ f2 position_delta2(const DevModel& m, const float* xs
     x = f2{xs[p[0]], xs[p[1]]};
   }
   lnew = lo + dl;
+  if constexpr (RV) {
+    // M71 with the 1/v cache: pix_delta2's operations, r0 read, v0 not formed
+    const f2 r0 = {rv[p[0]], rv[p[1]]};
+    const f2 v1 = fma2(lnew, m.eta, m.s0sq);
+    const f2 r1 = rcp2(v1);
+    rnew = r1;
+    const f2 d0 = x - lo, d1 = x - lnew;
+    const f2 t = fma2(d0 * d0, r0, -(d1 * d1) * r1);
+    return fma2(t, 0.5f, (-0.5f * kLn2) * log2_2(v1 * r0));
+  }
   f2 lgx = {0.f, 0.f};
   if constexpr (MODEL == SMCDET_MODEL_POISSON) lgx = f2{lg[p[0]], lg[p[1]]};
   return pix_delta2<MODEL>(m, x, lgx, lo, dl);
@@ -274,10 +297,16 @@ constexpr int mh_slots() { return PPL == 1 ? 1 : kSlots; }
 // updates in place; LDS holds only the workgroup counters.
 // PC: small tiles (PPL == 1, incremental) with the per-wave PSF cache in LDS
 // (S rows of H*W floats after the rate images; position_delta_pc).
+// RV: M71 tiles rendered in registers (PPL > 1, incremental, no fused tail):
+// a per-wave image of 1/v = 1/(s0^2 + eta*lambda) in LDS after the rate
+// images, so pix_delta reads the old pixel's reciprocal instead of forming it
+// (kept current on accept with the same operations: bit-identical).
 template <int MODEL, bool REPLAY, bool FULL, int PPL, bool PAIRED, bool TAIL, bool GL = false,
-          bool PC = false>
+          bool PC = false, bool RV = false>
 __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_kernel(MhArgs a) {
   static_assert(!PC || (PPL == 1 && !FULL && !GL && !TAIL), "PSF cache: small incremental tiles");
+  static_assert(!RV || (MODEL == SMCDET_MODEL_M71 && PPL > 1 && !FULL && !GL && !TAIL && PAIRED),
+                "1/v cache: M71 register-render tiles, incremental, paired");
   constexpr int NSL = mh_slots<PPL>();
   extern __shared__ float smem[];
   __shared__ int wg_acc, wg_done;  // last-iteration accepts / finished waves of this workgroup
@@ -383,6 +412,13 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     cur_ll = pixel_sum<MODEL>(m, xs, lg, lam, nullptr, lane);
   }
   lam[HW + lane] = m.bg;
+  [[maybe_unused]] float* rv = nullptr;
+  if constexpr (RV) {
+    rv = lam + kMhWaves * HWp;
+    wave_sync();
+    for (int p = lane; p < HWp; p += kWave) rv[p] = fast_rcp(fmaf(m.eta, lam[p], m.s0sq));
+    wave_sync();
+  }
   // the PSF cache: row s = source s's raw PSF at every pixel, 0 outside its
   // (2R+1)^2 window anchored at floor(loc) -- position_delta's old-window value
   [[maybe_unused]] float* pcw = nullptr;
@@ -565,6 +601,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     double new_ll = 0.0;
     float s_lam[NSL];
     int s_pix[NSL];
+    [[maybe_unused]] float s_rv[RV ? NSL : 1];  // RV: the new 1/v of each slot
     [[maybe_unused]] float s_psi = 0.f;  // PC: the new window's PSF values (one slot)
     int npos = 0, bw = 1, r0 = 0, c0 = 0, nslots = 0;
     if constexpr (FULL) {
@@ -611,15 +648,16 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           const int bb = q - (int)__umul24((unsigned)aa, (unsigned)bw);
           const int ph = r0 + aa, pw = c0 + bb;
           const int p = valid ? (int)__umul24((unsigned)ph, (unsigned)m.W) + pw : HW + lane;
-          float lnew, e;
+          float lnew, rnew, e;
           if constexpr (PC)
             e = position_delta_pc<MODEL, win>(m, xs, lg, lam, pcw + P.j * HW, p, valid, aa, bb, ph,
                                               pw, P, amp_o, amp_n, an_h, an_w, lnew, s_psi);
           else
-            e = position_delta<MODEL, win, GL>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o, amp_n,
-                                               ao_h, ao_w, an_h, an_w, lnew);
+            e = position_delta<MODEL, win, GL, RV>(m, xs, lg, lam, rv, p, aa, bb, ph, pw, P, amp_o,
+                                                   amp_n, ao_h, ao_w, an_h, an_w, lnew, rnew);
           acc += valid ? e : 0.f;
           s_lam[i] = lnew;
+          if constexpr (RV) s_rv[i] = rnew;
           s_pix[i] = p;
         }
         return acc;
@@ -647,14 +685,19 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
             fph[h] = (float)ph + 0.5f;
             fpw[h] = (float)pw + 0.5f;
           }
-          f2 lnew;
-          f2 e = position_delta2<MODEL, win, GL>(m, xs, lg, lam, p, aa, bb, fph, fpw, P, amp_o, amp_n,
-                                             ao_h, ao_w, an_h, an_w, lnew);
+          f2 lnew, rnew;
+          f2 e = position_delta2<MODEL, win, GL, RV>(m, xs, lg, lam, rv, p, aa, bb, fph, fpw, P,
+                                                     amp_o, amp_n, ao_h, ao_w, an_h, an_w, lnew,
+                                                     rnew);
           e.x = valid[0] ? e.x : 0.f;
           e.y = valid[1] ? e.y : 0.f;
           acc += e;
           s_lam[2 * i] = lnew.x;
           s_lam[2 * i + 1] = lnew.y;
+          if constexpr (RV) {
+            s_rv[2 * i] = rnew.x;
+            s_rv[2 * i + 1] = rnew.y;
+          }
           s_pix[2 * i] = p[0];
           s_pix[2 * i + 1] = p[1];
         }
@@ -666,11 +709,13 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           const int bb = q - (int)__umul24((unsigned)aa, (unsigned)bw);
           const int ph = r0 + aa, pw = c0 + bb;
           const int p = valid ? (int)__umul24((unsigned)ph, (unsigned)m.W) + pw : HW + lane;
-          float lnew;
-          const float e = position_delta<MODEL, win, GL>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o,
-                                                     amp_n, ao_h, ao_w, an_h, an_w, lnew);
+          float lnew, rnew;
+          const float e = position_delta<MODEL, win, GL, RV>(m, xs, lg, lam, rv, p, aa, bb, ph, pw,
+                                                         P, amp_o, amp_n, ao_h, ao_w, an_h, an_w,
+                                                         lnew, rnew);
           acc1 = valid ? e : 0.f;
           s_lam[2 * np] = lnew;
+          if constexpr (RV) s_rv[2 * np] = rnew;
           s_pix[2 * np] = p;
         }
         return (acc.x + acc.y) + acc1;
@@ -697,10 +742,13 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           const int bb = q - (int)__umul24((unsigned)aa, (unsigned)bw);
           const int ph = r0 + aa, pw = c0 + bb;
           const int p = (int)__umul24((unsigned)ph, (unsigned)m.W) + pw;
-          float lnew;
-          acc += position_delta<MODEL, true, GL>(m, xs, lg, lam, p, aa, bb, ph, pw, P, amp_o, amp_n,
-                                             ao_h, ao_w, an_h, an_w, lnew);
-          if constexpr (decltype(WRITE)::value) lam[p] = lnew;
+          float lnew, rnew;
+          acc += position_delta<MODEL, true, GL, RV>(m, xs, lg, lam, rv, p, aa, bb, ph, pw, P, amp_o,
+                                                     amp_n, ao_h, ao_w, an_h, an_w, lnew, rnew);
+          if constexpr (decltype(WRITE)::value) {
+            lam[p] = lnew;
+            if constexpr (RV) rv[p] = rnew;
+          }
         }
         return acc;
       };
@@ -721,7 +769,11 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
         if (accept && P.hast != -INFINITY) {
 #pragma unroll
           for (int i = 0; i < ns; ++i)
-            if (i < nslots) lam[s_pix[i]] = s_lam[i];
+            if (i < nslots) {
+              lam[s_pix[i]] = s_lam[i];
+              // the moved pixels' 1/v: the delta's own reciprocal of the new rate
+              if constexpr (RV) rv[s_pix[i]] = s_rv[i];
+            }
           if (kFar && npos > kSlots * kWave) (void)far_positions(std::true_type{});
           wave_sync();
         }
@@ -926,6 +978,18 @@ static int launch_mh1(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
       int rc = ensure_lds((const void*)kpc, lds_pc);
       if (rc) return rc;
       launch_sweep(kpc, grid, dim3(kMhBlock), lds_pc, st, a);
+      return SMCDET_OK;
+    }
+  }
+  if constexpr (MODEL == SMCDET_MODEL_M71 && PPL > 1 && !FULL) {
+    // M71 register-render tiles: the 1/v image (HWp floats per wave) where
+    // the 4 workgroups per CU of the 4-waves-per-SIMD sweep still fit LDS
+    const size_t lds_rv = lds + (size_t)kMhWaves * (a.m.H * a.m.W + kWave) * sizeof(float);
+    if (paired && !tail && !a.no_rcp_cache && 4 * (lds_rv + 1024) <= 160 * 1024) {
+      auto krv = mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, false, true>;
+      int rc = ensure_lds((const void*)krv, lds_rv);
+      if (rc) return rc;
+      launch_sweep(krv, grid, dim3(kMhBlock), lds_rv, st, a);
       return SMCDET_OK;
     }
   }
@@ -1140,6 +1204,7 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
   a.scalar_slots = (flags & SMCDET_MH_SCALAR_SLOTS) != 0;
   a.skip_done = (flags & SMCDET_MH_SKIP_DONE) != 0;
   a.no_psf_cache = (flags & SMCDET_MH_NO_PSF_CACHE) != 0;
+  a.no_rcp_cache = (flags & SMCDET_MH_NO_RCP_CACHE) != 0;
   rc = a.m.model == SMCDET_MODEL_M71
            ? launch_mh<SMCDET_MODEL_M71>(a, replay != nullptr, full, grid, lds, st)
            : launch_mh<SMCDET_MODEL_POISSON>(a, replay != nullptr, full, grid, lds, st);

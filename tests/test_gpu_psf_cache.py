@@ -1,4 +1,4 @@
-"""The small-tile PSF cache (tiles of <= 64 pixels, incremental MH): each wave
+"""The MH sweep's LDS caches.  Small tiles (<= 64 pixels, incremental MH): each wave
 keeps its particle's S raw PSF images in LDS, so a move reads the moved
 source's old PSF instead of re-evaluating it.  The cached values are the ones
 the uncached sweep computes (same operations on the same inputs), so whole
@@ -64,4 +64,31 @@ def test_psf_cache_poisson_8x8_run_is_bit_identical():
     img = model.sample(l, f)[0, 0, :, :, 0].contiguous()
     out = [_run(img, 8, p_basic_prior(8, 3, 3), p_basic_model(8), p_basic_mh(40), 512, 9, c)
            for c in (True, False)]
+    _assert_same(*out)
+
+
+NO_RCP_CACHE = 4096  # include/smcdet_hip.h
+
+
+@pytest.mark.parametrize("H,N", [(32, 1024), (16, 512)])
+def test_rcp_cache_m71_run_is_bit_identical(H, N):
+    """M71 tiles of 65..1024 pixels keep a per-wave image of 1/(s0^2 + eta*rate)
+    in LDS (read by the pixel delta instead of formed; on accept the delta's
+    own reciprocal of the new rate is stored): whole C2-geometry runs are
+    bit-identical with and without it (SMCDET_MH_NO_RCP_CACHE)."""
+    img = _m71_image(H, 31 + H, 1)
+    out = []
+    for flags in (0, NO_RCP_CACHE):
+        from smcdet_amd.sampler import SMCsampler
+        mh = p_m71_mh(100)
+        mh.debug_flags = flags
+        s = SMCsampler(img, H, p_m71_prior(H, 10, 10, counts_rate=0.003125), p_m71_model(H), mh,
+                       N, 0.5, "systematic", M71["flux_detection_threshold"], 200,
+                       print_every=10 ** 9, seed=13, device=DEV)
+        s.run()
+        torch.cuda.synchronize()
+        out.append({k: getattr(s, k).detach().cpu().numpy().copy()
+                     for k in ("temperature", "log_normalizing_constant", "ess", "locs", "fluxes",
+                               "loglik", "mutation_acc_rates")} | {"iter": np.array(s.iter)})
+    assert out[0]["iter"] >= 2
     _assert_same(*out)
