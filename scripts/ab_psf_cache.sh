@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-mkdir -p gpurun_out/ab_pc
+mkdir -p gpurun_out/ab_pc; echo "A/B flag ${AB_FLAG:-2048}"
 timeout -k 10 400 python -u -m pytest tests/test_gpu_psf_cache.py tests/test_gpu_parity.py \
   tests/test_gpu_fused_step.py -v -p no:cacheprovider --timeout 200 --timeout-method thread \
   > gpurun_out/ab_pc/pytest.log 2>&1
@@ -14,7 +14,7 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 Q="--no-cpu-baseline --no-full-run --no-vs-ref --no-spread"
 for rep in 1 2; do
   for wl in c4 c5; do
-    for fl in 0 2048; do
+    for fl in 0 ${AB_FLAG:-2048}; do
       timeout -k 10 200 python bench.py --workload $wl $Q --mh-debug-flags $fl \
         > gpurun_out/ab_pc/${wl}_f${fl}_r${rep}.json 2> gpurun_out/ab_pc/${wl}_f${fl}_r${rep}.err
       rc=$?; [ $rc -ne 0 ] && { echo "bench $wl $fl rc=$rc"; exit $rc; }
