@@ -76,7 +76,10 @@ def _run(which, cfg, image, seed, fused=True, persist=True):
     return dict(logZ=float(s.log_normalizing_constant.flatten()[0]), iters=s.iter,
                 ess_trace=esses, tau_trace=taus, final_ess=float(s.ess.flatten()[0]),
                 pruned_hist=hist / hist.sum(),
-                mean_total_flux=float(s.posterior_mean_total_flux(s.fluxes).flatten()[0]))
+                mean_total_flux=float(s.posterior_mean_total_flux(s.fluxes).flatten()[0]),
+                # the oracle's statistic (make_oracle_stats.py): the plain mean
+                # over the final resampled population
+                mean_total_flux_unweighted=float(s.fluxes.sum(-1).mean()))
 
 
 def _se(a, b):
@@ -188,7 +191,8 @@ def test_statistical_parity_c2_geometry(which):
         fe_ref = np.array([r["final_ess"] for r in rr])
         assert abs(fe.mean() - fe_ref.mean()) <= 3 * _se(fe, fe_ref), (fe.mean(), fe_ref.mean())
         assert abs(it.mean() - it_ref.mean()) <= max(3 * _se(it, it_ref), 0.5)
-        fl = np.array([r["mean_total_flux"] for r in runs])
+        fkey = "mean_total_flux_unweighted" if which.endswith("_oracle") else "mean_total_flux"
+        fl = np.array([r[fkey] for r in runs])
         fl_ref = np.array([r["mean_total_flux"] for r in rr])
         assert abs(fl.mean() - fl_ref.mean()) <= 3 * _se(fl, fl_ref), (fl.mean(), fl_ref.mean())
         if which.endswith("_oracle"):
