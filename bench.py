@@ -53,7 +53,7 @@ F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
 # rocprofv3 PMC summary of the C2 MH launch (scripts/profile.sh + scripts/pmc_summary.py):
 # FETCH_SIZE / WRITE_SIZE (HBM traffic), SQ VALU counts, GRBM_GUI_ACTIVE (effective clock),
 # and the sha1 of the library sources it was measured on
-PMC_FILE = "pmc_mh_r03.json"
+PMC_FILE = "pmc_mh_r04.json"
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions/s: 1 per SIMD per 4 cycles (measured 4.2)
 # measured SIMD issue cycles per wave-instruction (scripts/probe/isa_probe.hip, 4 waves/SIMD,
 # profiles/r01_s2_isa_probe.txt): plain VALU 4.2, transcendental 8.6, packed f32 6.0
@@ -64,6 +64,53 @@ SIMD_CYCLES_PER_S = 256 * 4 * 2.4e9
 REFERENCE_CPU = {"value": 8466.0, "unit": "particle-steps/sec", "cores": 8, "kind": "reference",
                  "sample": "reference SingleComponentMH, 32x32, N=4096, S=10, 10 iterations at "
                            "tau=0.3, torch 2.10 CPU float32 (SURVEY.md §6)"}
+
+
+# --host-rehearsal: the multi-rank bookkeeping on the CPU (gloo, stub sampler)
+REHEARSAL = False
+
+
+def _sync():
+    """torch.cuda.synchronize(), or nothing in a CPU host rehearsal."""
+    if not REHEARSAL:
+        torch.cuda.synchronize()
+
+
+class RehearsalSampler:
+    """The SMCsampler surface bench.py drives (initialize, _temper_reweight,
+    _step, the state tensors and _T), on the CPU with no kernel: a step sleeps
+    1 ms per tile and rank, so ranks finish at different times and the MAX
+    over ranks is what the line reports.  For tests/test_bench_host.py's
+    2-rank gloo torchrun of bench.py (--host-rehearsal)."""
+
+    def __init__(self, T, N, S, rank):
+        self._T, self.N, self.S, self.rank = T, N, S, rank
+        self.device = torch.device("cpu")
+        self.fused_step = False
+        self.temperature = torch.zeros(1, T)
+        self.ess = torch.full((1, T), float(N))
+        self.mutation_acc_rates = torch.zeros(1, T)
+        self.counts = torch.full((1, T, N), float(S))
+        self.locs = torch.zeros(1, T, N, S, 2)
+        self.fluxes = torch.ones(1, T, N, S)
+        self.weights = torch.full((1, T, N), 1.0 / N)
+        self.log_normalizing_constant = torch.zeros(1, T)
+        self._pending_idx = None
+        self.steps_run = 0
+
+    def initialize(self):
+        pass
+
+    def _step_fusable(self):
+        return False
+
+    def _temper_reweight(self, with_resample=True):
+        self._pending_idx = torch.arange(self.N).repeat(1, self._T, 1)
+
+    def _step(self, idx):
+        time.sleep(1e-3 * self._T * (1 + self.rank))
+        self.steps_run += 1
+        self._temper_reweight(True)
 
 
 def parse():
@@ -114,6 +161,10 @@ def parse():
     ap.add_argument("--no-spread", action="store_true")
     # diagnostic MH flags (A/B timing: e.g. 2048 = SMCDET_MH_NO_PSF_CACHE)
     ap.add_argument("--mh-debug-flags", type=int, default=0)
+    # CPU rehearsal of the multi-rank bookkeeping (gloo, RehearsalSampler: no
+    # GPU, no kernel): shard sizes, the barrier + MAX-over-ranks timing, the
+    # rank-0-only line / vs_reference / cpu_baseline, the catalog gather
+    ap.add_argument("--host-rehearsal", action="store_true")
     return ap.parse_args()
 
 
@@ -227,8 +278,17 @@ def cpu_baseline(args, image_tile, seconds):
 
 def build_sampler(args, dev, rank):
     """(sampler, particle-steps per SMC step, workload description)."""
-    from smcdet_amd.sampler import SMCsampler
     p = M71
+    if REHEARSAL:
+        H, S, Np, K = args.tile, args.sources, args.particles, args.mh_iters
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        ids = shard(args.total_tiles, world, rank) if args.total_tiles > 0 else [rank]
+        T = len(ids)
+        return RehearsalSampler(T, Np, S, rank), None, T * Np * K, torch.zeros(H, H), dict(
+            workload=f"host rehearsal: {T} stub tile(s) on rank {rank} of {world}",
+            total_tiles=args.total_tiles, tiles_per_gpu=T, particles=Np, tile=H, sources=S,
+            mh_iters=K, kernel=args.kernel, tile_ids=ids)
+    from smcdet_amd.sampler import SMCsampler
     if args.workload == "c2" and args.total_tiles > 0:
         H, S, Np, K = args.tile, args.sources, args.particles, args.mh_iters
         world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -450,6 +510,8 @@ def pmc_summary(args):
     stale: its counters do not describe this run's kernel."""
     if args.workload != "c2" or args.kernel != "mh" or args.full_recompute:
         return None, "no PMC summary for this workload"
+    if REHEARSAL:
+        return None, "host rehearsal (no kernel)"
     path = os.path.join(ROOT, "profiles", PMC_FILE)
     if not os.path.exists(path):
         return None, f"profiles/{PMC_FILE} missing"
@@ -630,14 +692,14 @@ def c3_leg(args, dev, rank, world, dist, backend):
     steps = max(3, min(args.steps, 10))
     for _ in range(2):
         step()
-    torch.cuda.synchronize()
+    _sync()
     if dist:
         tdist.barrier()
-    torch.cuda.synchronize()
+    _sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
-    torch.cuda.synchronize()
+    _sync()
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
@@ -670,11 +732,11 @@ def catalog_gather(s, rank, world, dist, backend):
              "ess": s.ess.reshape(T)}
     nbytes = sum(v.numel() * v.element_size() for v in local.values())
     gather_tile_results(local, C3_TILES, 8, rank, world)  # warm-up (communicator setup)
-    torch.cuda.synchronize()
+    _sync()
     tdist.barrier()
     t0 = time.perf_counter()
     out = gather_tile_results(local, C3_TILES, 8, rank, world)
-    torch.cuda.synchronize()
+    _sync()
     tdist.barrier()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], device=s.device if backend == "nccl" else "cpu", dtype=torch.float64)
@@ -697,7 +759,12 @@ def _hip_fused(s):
 
 
 def main():
+    global REHEARSAL
     args = parse()
+    if args.host_rehearsal:
+        REHEARSAL = True
+        os.environ["SMCDET_DIST_BACKEND"] = "gloo"
+        args.no_kernel_timing = args.no_full_run = args.no_cpu_baseline = True
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -713,13 +780,17 @@ def main():
     backend = os.environ.get("SMCDET_DIST_BACKEND", "nccl")
     if dist:
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
+        if not REHEARSAL:
+            torch.cuda.set_device(local)
         if backend == "nccl":
             tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             tdist.init_process_group(backend)
-    dev = torch.device("cuda", local if dist else 0)
-    torch.cuda.set_device(dev)
+    if REHEARSAL:
+        dev = torch.device("cpu")
+    else:
+        dev = torch.device("cuda", local if dist else 0)
+        torch.cuda.set_device(dev)
 
     if args.workload not in ("c2", "agg") and args.tiles_per_gpu == 1:
         args.tiles_per_gpu = 42  # 332 M71 cutouts over 8 GPUs (manuscript.tex:562)
@@ -747,14 +818,14 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    _sync()
     if dist:
         tdist.barrier()
-    torch.cuda.synchronize()
+    _sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    _sync()
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
@@ -772,7 +843,7 @@ def main():
         _hip.launch_timing(args.steps)
         for _ in range(args.steps):
             step()
-        torch.cuda.synchronize()
+        _sync()
         ev = _hip.launch_timing_read(args.steps)
         starts = _hip.launch_timing_starts(args.steps)
         _hip.launch_timing(0)
@@ -780,11 +851,11 @@ def main():
     # and the launch-to-launch intervals of the timing pass above
     passes = []
     for _ in range(0 if args.no_spread else 3):
-        torch.cuda.synchronize()
+        _sync()
         t1 = time.perf_counter()
         for _ in range(args.steps):
             step()
-        torch.cuda.synchronize()
+        _sync()
         passes.append((time.perf_counter() - t1) / args.steps * 1e3)
     if dist:
         t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu",
@@ -886,11 +957,14 @@ def main():
                            ("vs_reference_k20", "c2_moderate_4096"),
                            ("vs_reference_n512", "c2_moderate")):
             try:
-                r = vs_reference(dev, which)
+                r = ({"rehearsal": f"vs_reference({which}) on rank {rank}"} if REHEARSAL
+                     else vs_reference(dev, which))
             except Exception as e:  # report, never fail the bench line on it
                 r = {"error": repr(e)}
             if r is not None:
                 out["smc"][key] = r
+    if REHEARSAL and rank == 0 and world == 1:
+        out["cpu_baseline"] = {"rehearsal": f"cpu_baseline on rank {rank}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
         try:
             out["cpu_baseline"] = cpu_baseline(args, cpu_tile.cpu().numpy(),

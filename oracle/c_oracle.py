@@ -108,6 +108,33 @@ def mh_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mh, replay=No
     return (l, f, rate, acc == 2) if frozen_out else (l, f, rate)
 
 
+def sweep_draws(seed, T, N, K, S):
+    """The draws mh_oracle_sweep makes from its own stream when no replay
+    arrays are given (oracle/mh_oracle.c: splitmix64 per particle, state
+    seed ^ 0xA5A5A5A5 (pid + 1); per iteration the component, then the h, w,
+    flux and accept uniforms, 24-bit, exact in float32), as replay arrays
+    comp [K,T,N] int32, uloc [K,T,N,2], uflux / uacc [K,T,N] float32: a
+    sweep replaying them makes the same decisions as the seeded sweep (the
+    paired replays of tests/test_gpu_paired.py)."""
+    u64 = np.uint64
+    pid = np.arange(T * N, dtype=np.uint64)
+    st = u64(seed) ^ (u64(0xA5A5A5A5) * (pid + u64(1)))
+    out = np.empty((K, 5, T * N), np.float64)
+    with np.errstate(over="ignore"):
+        for k in range(K):
+            for d in range(5):
+                st = st + u64(0x9E3779B97F4A7C15)
+                z = (st ^ (st >> u64(30))) * u64(0xBF58476D1CE4E5B9)
+                z = (z ^ (z >> u64(27))) * u64(0x94D049BB133111EB)
+                z = z ^ (z >> u64(31))
+                out[k, d] = (z >> u64(40)).astype(np.float64) * (1.0 / 16777216.0)
+    comp = np.minimum((out[:, 0] * S).astype(np.int32), S - 1)
+    return {"comp": comp.reshape(K, T, N),
+            "uloc": np.stack([out[:, 1], out[:, 2]], -1).astype(np.float32).reshape(K, T, N, 2),
+            "uflux": out[:, 3].astype(np.float32).reshape(K, T, N),
+            "uacc": out[:, 4].astype(np.float32).reshape(K, T, N)}
+
+
 def loglik(tiled_image, locs, fluxes, model, threads=0):
     """Image log-likelihoods [nH,nW,N] (float64) of the catalogs, by the C
     restatement (images.py:159-175 / :85-102)."""

@@ -2,7 +2,7 @@
 # One GPU pass of a session: the GPU suite, smoke, the default bench line, the
 # driver's torchrun N=1 path (RCCL process group of one rank), and the
 # rocprofv3 kernel-trace + PMC passes of the C2 MH launch summarised into
-# gpurun_out/pmc_mh_r03.json (scripts/pmc_summary.py).  Each GPU step has its
+# gpurun_out/pmc_mh_r04.json (scripts/pmc_summary.py).  Each GPU step has its
 # own time limit; a crash, abort or timeout ends the script (test failures,
 # rc 1, do not).  STEPS="pytest smoke bench torchrun1 profile" selects steps.
 set -u
@@ -44,7 +44,7 @@ if has host; then  # host-side issue cost of a step vs its GPU time
   cat gpurun_out/host_overhead.json
 fi
 if has profile; then
-  OUT=gpurun_out/prof SUMMARY=gpurun_out/pmc_mh_r03.json \
+  OUT=gpurun_out/prof SUMMARY=gpurun_out/pmc_mh_r04.json \
     SQ="SQ_INSTS_VALU SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP32_TRANS SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_INSTS_SMEM" \
     bash scripts/profile.sh
   step profile $?

@@ -157,6 +157,98 @@ _SIGS = {
 }
 EXPORTS = tuple(_SIGS)
 
+# Output arguments (0-based positions) of each entry point, and the in-place
+# pairs the header allows (an input buffer that is also the output: the MH /
+# MALA / aggregation sweeps without an ancestor gather, a sampled image
+# written over its rate image).  Every call through lib() rejects any other
+# output pointer that equals another argument's pointer: two arguments in one
+# buffer is what a freed temporary reused by the caching allocator looks like
+# (round 3: test_tile_pass_4096_vs_reference read every weight as 1/N).
+_SWEEP_OUTS = (12, 13, 14, 16, 21, 22, 23)
+_SWEEP_INPLACE = ((9, 12), (10, 13), (11, 14), (15, 16))
+_OUTS = {
+    "smcdet_loglik": ((7,), ()),
+    "smcdet_render": ((6,), ()),
+    "smcdet_psf_dense": ((5,), ()),
+    "smcdet_sample_image": ((5,), ((1, 5),)),
+    "smcdet_log_prior": ((8,), ()),
+    "smcdet_prior_sample": ((8, 9, 10), ()),
+    "smcdet_mh_sweep": (_SWEEP_OUTS, _SWEEP_INPLACE),
+    "smcdet_mh_sweep_step": (_SWEEP_OUTS, _SWEEP_INPLACE),
+    "smcdet_mala_sweep": (_SWEEP_OUTS, _SWEEP_INPLACE),
+    "smcdet_mh_chain": ((8, 9, 18, 19, 20, 21), ()),
+    "smcdet_temper": ((1, 2), ()),
+    "smcdet_update_weights": ((3, 4, 5, 6), ()),
+    "smcdet_resample_index": ((7,), ()),
+    "smcdet_temper_reweight": ((1, 2, 3, 4, 5, 6, 13, 15, 17), ()),
+    "smcdet_gather": ((7, 8, 9), ()),
+    "smcdet_count_posterior": ((16, 17, 18, 19, 20), ()),
+    "smcdet_prune": ((7, 8, 9), ()),
+    "smcdet_aggregate_sweep": ((13, 14, 15, 19, 20, 21, 22, 24), ((10, 13), (11, 14), (12, 15))),
+    "smcdet_aggregate_temper": ((10,), ()),
+    "smcdet_aggregate_reweight": ((10, 11, 12, 13, 17), ()),
+}
+
+
+def _addr(a):
+    if isinstance(a, ctypes.c_void_p):
+        return a.value or 0
+    if isinstance(a, int) and not isinstance(a, bool):
+        return a
+    return 0
+
+
+def check_aliases(name, args):
+    """ValueError if an output argument of `name` shares its pointer with
+    another argument (other than the header's in-place pairs); the stream (last
+    argument) is not compared."""
+    spec = _OUTS.get(name)
+    if spec is None:
+        return
+    outs, inplace = spec
+    ok = {frozenset(pq) for pq in inplace}
+    addrs = [_addr(a) for a in args[:-1]]
+    for o in outs:
+        if o >= len(addrs) or not addrs[o]:
+            continue
+        for i, v in enumerate(addrs):
+            if i != o and v == addrs[o] and frozenset((i, o)) not in ok:
+                raise ValueError(
+                    f"{name}: argument {o} (an output) and argument {i} are the same device "
+                    f"pointer 0x{v:x}; every buffer passed to the C ABI must be its own "
+                    "allocation and stay referenced until the launch's stream has passed it "
+                    "(a freed temporary reused by PyTorch's caching allocator looks like this; "
+                    "INTEGRATION.md §4)")
+
+
+class _Checked:
+    """An entry point that checks its pointer arguments before the call."""
+
+    def __init__(self, fn, name):
+        self._fn, self._name = fn, name
+
+    def __call__(self, *args):
+        check_aliases(self._name, args)
+        return self._fn(*args)
+
+    def __getattr__(self, k):
+        return getattr(self._fn, k)
+
+
+class _Lib:
+    """libsmcdet_hip.so with alias-checked entry points (check_aliases);
+    anything else is the CDLL's own attribute."""
+
+    def __init__(self, cdll):
+        self._cdll = cdll
+        for name in _OUTS:
+            if hasattr(cdll, name):
+                setattr(self, name, _Checked(getattr(cdll, name), name))
+
+    def __getattr__(self, k):
+        return getattr(self._cdll, k)
+
+
 _lib = None
 
 # the library's sources in the Makefile's SRCS + HDRS order: their sha1 is
@@ -211,7 +303,7 @@ def lib():
                 raise RuntimeError(
                     f"smcdet_amd: {LIB_PATH} was built from sources with sha1 {built}, the "
                     f"sources here hash to {src}: rebuild with `make`")
-        _lib = L
+        _lib = _Lib(L)
     return _lib
 
 
@@ -250,8 +342,21 @@ def launch_timing_starts(max_launches: int):
     return [float(buf[i]) for i in range(min(n.value, int(max_launches)))]
 
 
+# ptr() keeps the last _KEEP tensors it converted alive, so a temporary passed
+# as `ptr(torch.tensor(...))` outlives the call it is an argument of (and its
+# block cannot be handed to the next temporary of the same call)
+_KEEP = 256
+_kept = [None] * _KEEP
+_kept_i = 0
+
+
 def ptr(t):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    global _kept_i
+    if t is None:
+        return None
+    _kept[_kept_i] = t
+    _kept_i = (_kept_i + 1) % _KEEP
+    return ctypes.c_void_p(t.data_ptr())
 
 
 def stream_of(t) -> ctypes.c_void_p:

@@ -335,6 +335,10 @@ __global__ __launch_bounds__(kAggMaxWaves* kWave) void agg_sweep_kernel(AggArgs 
 
 using namespace smcdet;
 
+// fewest waves per workgroup the LDS aggregation sweep runs with (above: the
+// workspace variant, M71 only)
+static int agg_min_lds_waves(int model) { return model == SMCDET_MODEL_M71 ? 2 : 1; }
+
 extern "C" int64_t smcdet_aggregate_workspace(const smcdet_image_model_t* model, int32_t T,
                                               int32_t N, int32_t S) {
   int rc = validate_model(model, kMaxGlobalPixels);
@@ -345,7 +349,11 @@ extern "C" int64_t smcdet_aggregate_workspace(const smcdet_image_model_t* model,
   const size_t HWp = (size_t)model->H * model->W + kWave;
   const size_t img_b = (model->model == SMCDET_MODEL_POISSON ? 2 : 1) * HWp * sizeof(float);
   const size_t wave_b = (2 * HWp + 3 * (size_t)S) * sizeof(float);
-  if (img_b + kAggMaxWaves * wave_b <= 160 * 1024) return 0;  // LDS path
+  // LDS path at the largest wave count (4..kAggMinLdsWaves) whose workgroup
+  // fits; the workspace only beyond that (M71: the global-memory variant
+  // keeps 4 waves per workgroup where LDS would hold one, i.e. one wave per
+  // CU; the Poisson model has no such variant and goes down to one wave)
+  if (img_b + agg_min_lds_waves(model->model) * wave_b <= 160 * 1024) return 0;
   if (model->model != SMCDET_MODEL_M71)
     return set_error(SMCDET_EUNSUPPORTED, "joint tile %dx%d with S=%d exceeds LDS (M71 only "
                      "beyond)", model->H, model->W, S);
@@ -439,12 +447,14 @@ extern "C" int smcdet_aggregate_sweep(
       hipLaunchKernelGGL((agg_sweep_kernel<SMCDET_MODEL_M71, false, true>), grid, block, 0, st, a);
     return check_launch("smcdet_aggregate_sweep");
   }
-  // 4 waves per workgroup (smcdet_aggregate_workspace sends joint tiles that
-  // do not fit at 4 waves to the global-memory path)
+  // the largest wave count per workgroup (4..1) whose LDS fits
+  // (smcdet_aggregate_workspace sends joint tiles where not even one wave fits
+  // to the global-memory path, M71 only)
   const size_t HWp = (size_t)model->H * model->W + kWave;
   const size_t img_b = (model->model == SMCDET_MODEL_POISSON ? 2 : 1) * HWp * sizeof(float);
   const size_t wave_b = (2 * HWp + 3 * (size_t)S) * sizeof(float);
-  const int nw = kAggMaxWaves;
+  int nw = kAggMaxWaves;
+  while (nw > agg_min_lds_waves(model->model) && img_b + nw * wave_b > 160 * 1024) --nw;
   const size_t lds = img_b + nw * wave_b;
   a.nw = nw;
   const dim3 grid((N + nw - 1) / nw, T), block(nw * kWave);

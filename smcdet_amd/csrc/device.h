@@ -391,6 +391,52 @@ __device__ __forceinline__ f2 psf_raw2(const DevModel& m, f2 r2) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// M71 PSF as a radial table in LDS (the MH sweep's union-window deltas): the
+// raw profile psi(r^2) of psf_raw (images.py:137-141) as one cubic per node
+// of a uniform grid in r^2, node i centred at r^2 = i*h, t = r^2/h - i in
+// [-1/2, 1/2] (round to nearest).  The coefficients are fitted on the host in
+// double precision (psf_table_build, mh_kernel.hip) and stored as float4
+// (c0, c1, c2, c3); psi = c0 + t(c1 + t(c2 + t c3)).  One ds_read_b128 and
+// four VALU replace 3 exp2 + 1 log2 per evaluation; the fit error is below
+// float32 rounding (max relative error 3.0e-7, mean 9e-8, against 7.5e-7 /
+// 1.6e-7 for the float32 exp2/log2 form).
+// The index comes from the float32 round-to-nearest trick: y = u + 1.5*2^23
+// holds round(u) in its low mantissa bits (u < 2^22), y - 1.5*2^23 is that
+// integer exactly, so t is exact too.  CLAMP bounds the index for positions
+// outside the source's window (union windows of moved anchors: their value is
+// discarded, only the LDS address must stay inside the table).
+// ---------------------------------------------------------------------------
+constexpr int kTabIntervals = 512;
+constexpr int kTabNodes = kTabIntervals + 1;
+constexpr float kRoundMagic = 12582912.0f;  // 1.5 * 2^23
+constexpr int kRoundMagicBits = 0x4B400000;
+
+template <bool CLAMP>
+__device__ __forceinline__ float psf_tab(const float4* tab, float inv_h, float r2) {
+  const float u = r2 * inv_h;
+  const float y = u + kRoundMagic;
+  const float t = u - (y - kRoundMagic);
+  int i = __float_as_int(y) - kRoundMagicBits;
+  if (CLAMP) i = min(i, kTabIntervals);
+  const float4 c = tab[i];
+  return fmaf(fmaf(fmaf(c.w, t, c.z), t, c.y), t, c.x);
+}
+template <bool CLAMP>
+__device__ __forceinline__ f2 psf_tab2(const float4* tab, float inv_h, f2 r2) {
+  const f2 u = r2 * inv_h;
+  const f2 y = u + kRoundMagic;
+  const f2 t = u - (y - kRoundMagic);
+  int i0 = __float_as_int(y.x) - kRoundMagicBits, i1 = __float_as_int(y.y) - kRoundMagicBits;
+  if (CLAMP) {
+    i0 = min(i0, kTabIntervals);
+    i1 = min(i1, kTabIntervals);
+  }
+  const float4 c0 = tab[i0], c1 = tab[i1];
+  return f2{fmaf(fmaf(fmaf(c0.w, t.x, c0.z), t.x, c0.y), t.x, c0.x),
+            fmaf(fmaf(fmaf(c1.w, t.y, c1.z), t.y, c1.y), t.y, c1.x)};
+}
+
 template <int MODEL>
 __device__ __forceinline__ f2 pix_delta2(const DevModel& m, f2 x, f2 lgx, f2 lam, f2 dl) {
   if constexpr (MODEL == SMCDET_MODEL_M71) {

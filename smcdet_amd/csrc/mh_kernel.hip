@@ -33,8 +33,13 @@
 // wave-uniform about an iteration (anchors, amplitudes, prior and Hastings
 // terms) is computed once per proposal batch in the batch's lanes.
 #include <math.h>
+#include <string.h>
 
+#include <algorithm>
+#include <cmath>
+#include <mutex>
 #include <type_traits>
+#include <vector>
 
 #include "render.h"
 #include "tile.h"
@@ -63,6 +68,8 @@ struct MhArgs {
   int skip_done;                     // SMCDET_MH_SKIP_DONE
   int no_psf_cache;                  // SMCDET_MH_NO_PSF_CACHE (diagnostic)
   int no_rcp_cache;                  // SMCDET_MH_NO_RCP_CACHE (diagnostic)
+  const float4* psf_tab;             // M71 radial PSF table [kTabNodes] (or null: exp2/log2)
+  float tab_inv_h;                   // 1 / its node spacing in r^2
   const float* img;                  // [T,H,W]
   const float* temperature;          // [T]
   const int64_t* ancestors;          // [T,N] or null
@@ -153,19 +160,26 @@ __device__ __forceinline__ void propose_lane(float mu, float c_ph, float c_lZ, f
 // position of the (clipped) box is in both.
 // GL: the tile image lives in global memory (tiles above the LDS budget): a
 // masked lane's dummy position HW + lane reads the last pixel instead
-template <int MODEL, bool WINDOWS, bool GL = false, bool RV = false>
+// TB: the PSF values from the radial table in LDS (psf_tab, device.h)
+template <int MODEL, bool WINDOWS, bool GL = false, bool RV = false, bool TB = false>
 __device__ __forceinline__ float position_delta(const DevModel& m, const float* xs,
                                                 const float* lg, const float* lam,
-                                                const float* rv, int p,
-                                                int aa, int bb, int ph, int pw,
+                                                const float* rv, const float4* tab, float tinv,
+                                                int p, int aa, int bb, int ph, int pw,
                                                 const Proposal& P, float amp_o, float amp_n,
                                                 int ao_h, int ao_w, int an_h, int an_w,
                                                 float& lnew, float& rnew) {
   const float fph = (float)ph + 0.5f, fpw = (float)pw + 0.5f;
   const float dho = fph - P.h, dwo = fpw - P.w;
   const float dhn = fph - P.hn, dwn = fpw - P.wn;
-  float psi_o = psf_raw<MODEL>(m, fmaf(dho, dho, dwo * dwo));
-  float psi_n = psf_raw<MODEL>(m, fmaf(dhn, dhn, dwn * dwn));
+  float psi_o, psi_n;
+  if constexpr (TB) {
+    psi_o = psf_tab<WINDOWS>(tab, tinv, fmaf(dho, dho, dwo * dwo));
+    psi_n = psf_tab<WINDOWS>(tab, tinv, fmaf(dhn, dhn, dwn * dwn));
+  } else {
+    psi_o = psf_raw<MODEL>(m, fmaf(dho, dho, dwo * dwo));
+    psi_n = psf_raw<MODEL>(m, fmaf(dhn, dhn, dwn * dwn));
+  }
   if (WINDOWS) {
     const unsigned span = 2u * (unsigned)m.R;
     psi_o = ((unsigned)(aa - ao_h) <= span && (unsigned)(bb - ao_w) <= span) ? psi_o : 0.f;
@@ -193,17 +207,24 @@ __device__ __forceinline__ float position_delta(const DevModel& m, const float* 
 // arithmetic runs as packed v_pk_{fma,mul,add}_f32 (one issue for both
 // halves), the transcendentals per half.  Same per-element operation order as
 // position_delta.
-template <int MODEL, bool WINDOWS, bool GL = false, bool RV = false>
+template <int MODEL, bool WINDOWS, bool GL = false, bool RV = false, bool TB = false>
 __device__ __forceinline__ f2 position_delta2(const DevModel& m, const float* xs, const float* lg,
-                                             const float* lam, const float* rv, const int (&p)[2],
+                                             const float* lam, const float* rv,
+                                             const float4* tab, float tinv, const int (&p)[2],
                                              const int (&aa)[2], const int (&bb)[2], f2 fph,
                                              f2 fpw, const Proposal& P, float amp_o, float amp_n,
                                              int ao_h, int ao_w, int an_h, int an_w, f2& lnew,
                                              f2& rnew) {
   const f2 dho = fph - P.h, dwo = fpw - P.w;
   const f2 dhn = fph - P.hn, dwn = fpw - P.wn;
-  f2 psi_o = psf_raw2<MODEL>(m, fma2(dho, dho, dwo * dwo));
-  f2 psi_n = psf_raw2<MODEL>(m, fma2(dhn, dhn, dwn * dwn));
+  f2 psi_o, psi_n;
+  if constexpr (TB) {
+    psi_o = psf_tab2<WINDOWS>(tab, tinv, fma2(dho, dho, dwo * dwo));
+    psi_n = psf_tab2<WINDOWS>(tab, tinv, fma2(dhn, dhn, dwn * dwn));
+  } else {
+    psi_o = psf_raw2<MODEL>(m, fma2(dho, dho, dwo * dwo));
+    psi_n = psf_raw2<MODEL>(m, fma2(dhn, dhn, dwn * dwn));
+  }
   if (WINDOWS) {
     const unsigned span = 2u * (unsigned)m.R;
 #pragma unroll
@@ -246,17 +267,20 @@ __device__ __forceinline__ f2 position_delta2(const DevModel& m, const float* xs
 // position_delta computes, by the same operations on the same inputs (the
 // cached row was evaluated at the source's current position), so decisions
 // and rates are bit-identical to the uncached sweep.
-template <int MODEL, bool WINDOWS>
+template <int MODEL, bool WINDOWS, bool TB = false>
 __device__ __forceinline__ float position_delta_pc(const DevModel& m, const float* xs,
                                                    const float* lg, const float* lam,
-                                                   const float* pcj, int p, bool valid, int aa,
+                                                   const float* pcj, const float4* tab,
+                                                   float tinv, int p, bool valid, int aa,
                                                    int bb, int ph, int pw, const Proposal& P,
                                                    float amp_o, float amp_n, int an_h, int an_w,
                                                    float& lnew, float& psi_new) {
   const float fph = (float)ph + 0.5f, fpw = (float)pw + 0.5f;
   const float dhn = fph - P.hn, dwn = fpw - P.wn;
   const float psi_o = pcj[valid ? p : 0];  // (a masked lane's value is discarded)
-  float psi_n = psf_raw<MODEL>(m, fmaf(dhn, dhn, dwn * dwn));
+  float psi_n;
+  if constexpr (TB) psi_n = psf_tab<WINDOWS>(tab, tinv, fmaf(dhn, dhn, dwn * dwn));
+  else psi_n = psf_raw<MODEL>(m, fmaf(dhn, dhn, dwn * dwn));
   if (WINDOWS) {
     const unsigned span = 2u * (unsigned)m.R;
     psi_n = ((unsigned)(aa - an_h) <= span && (unsigned)(bb - an_w) <= span) ? psi_n : 0.f;
@@ -301,12 +325,17 @@ constexpr int mh_slots() { return PPL == 1 ? 1 : kSlots; }
 // a per-wave image of 1/v = 1/(s0^2 + eta*lambda) in LDS after the rate
 // images, so pix_delta reads the old pixel's reciprocal instead of forming it
 // (kept current on accept with the same operations: bit-identical).
+// TB: M71 incremental sweeps with the radial PSF table (psf_tab, device.h)
+// staged into LDS after the images / caches: every union-window PSF value
+// (and the PSF cache's rows) comes from the table.
 template <int MODEL, bool REPLAY, bool FULL, int PPL, bool PAIRED, bool TAIL, bool GL = false,
-          bool PC = false, bool RV = false>
+          bool PC = false, bool RV = false, bool TB = false>
 __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_kernel(MhArgs a) {
   static_assert(!PC || (PPL == 1 && !FULL && !GL && !TAIL), "PSF cache: small incremental tiles");
   static_assert(!RV || (MODEL == SMCDET_MODEL_M71 && PPL > 1 && !FULL && !GL && !TAIL && PAIRED),
                 "1/v cache: M71 register-render tiles, incremental, paired");
+  static_assert(!TB || (MODEL == SMCDET_MODEL_M71 && PPL > 0 && !FULL && !GL && !TAIL && PAIRED),
+                "PSF table: M71 register-render tiles, incremental, paired");
   constexpr int NSL = mh_slots<PPL>();
   extern __shared__ float smem[];
   __shared__ int wg_acc, wg_done;  // last-iteration accepts / finished waves of this workgroup
@@ -338,6 +367,16 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   if (!GL && threadIdx.x < kWave) {
     xs[HW + threadIdx.x] = m.bg;
     if (MODEL == SMCDET_MODEL_POISSON) lg[HW + threadIdx.x] = 0.f;
+  }
+  // the radial PSF table, 16-B aligned after the images and caches
+  [[maybe_unused]] const float4* tab = nullptr;
+  [[maybe_unused]] const float tinv = a.tab_inv_h;
+  if constexpr (TB) {
+    const int off = ((kImg + kMhWaves) * HWp + (RV ? kMhWaves * HWp : 0) +
+                     (PC ? kMhWaves * a.S * HW : 0) + 3) & ~3;
+    float4* t4 = reinterpret_cast<float4*>(smem + off);
+    for (int i = threadIdx.x; i < kTabNodes; i += kMhBlock) t4[i] = a.psf_tab[i];
+    tab = t4;
   }
   __syncthreads();
   SMC_TRACE(trow, 1);
@@ -430,7 +469,9 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
       const float hs = readlane(sh, s), ws = readlane(sw, s);
       const int fh = ifloor16(hs), fw = ifloor16(ws);
       const float dh = fph - hs, dw = fpw - ws;
-      const float v = psf_raw<MODEL>(m, fmaf(dh, dh, dw * dw));
+      float v;
+      if constexpr (TB) v = psf_tab<true>(tab, tinv, fmaf(dh, dh, dw * dw));
+      else v = psf_raw<MODEL>(m, fmaf(dh, dh, dw * dw));
       if (lane < HW) pcw[s * HW + lane] = (abs(ph - fh) <= m.R && abs(pw - fw) <= m.R) ? v : 0.f;
     }
     wave_sync();
@@ -650,11 +691,13 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           const int p = valid ? (int)__umul24((unsigned)ph, (unsigned)m.W) + pw : HW + lane;
           float lnew, rnew, e;
           if constexpr (PC)
-            e = position_delta_pc<MODEL, win>(m, xs, lg, lam, pcw + P.j * HW, p, valid, aa, bb, ph,
-                                              pw, P, amp_o, amp_n, an_h, an_w, lnew, s_psi);
+            e = position_delta_pc<MODEL, win, TB>(m, xs, lg, lam, pcw + P.j * HW, tab, tinv, p,
+                                                  valid, aa, bb, ph, pw, P, amp_o, amp_n, an_h,
+                                                  an_w, lnew, s_psi);
           else
-            e = position_delta<MODEL, win, GL, RV>(m, xs, lg, lam, rv, p, aa, bb, ph, pw, P, amp_o,
-                                                   amp_n, ao_h, ao_w, an_h, an_w, lnew, rnew);
+            e = position_delta<MODEL, win, GL, RV, TB>(m, xs, lg, lam, rv, tab, tinv, p, aa, bb,
+                                                       ph, pw, P, amp_o, amp_n, ao_h, ao_w, an_h,
+                                                       an_w, lnew, rnew);
           acc += valid ? e : 0.f;
           s_lam[i] = lnew;
           if constexpr (RV) s_rv[i] = rnew;
@@ -686,9 +729,9 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
             fpw[h] = (float)pw + 0.5f;
           }
           f2 lnew, rnew;
-          f2 e = position_delta2<MODEL, win, GL, RV>(m, xs, lg, lam, rv, p, aa, bb, fph, fpw, P,
-                                                     amp_o, amp_n, ao_h, ao_w, an_h, an_w, lnew,
-                                                     rnew);
+          f2 e = position_delta2<MODEL, win, GL, RV, TB>(m, xs, lg, lam, rv, tab, tinv, p, aa, bb,
+                                                         fph, fpw, P, amp_o, amp_n, ao_h, ao_w,
+                                                         an_h, an_w, lnew, rnew);
           e.x = valid[0] ? e.x : 0.f;
           e.y = valid[1] ? e.y : 0.f;
           acc += e;
@@ -710,9 +753,9 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           const int ph = r0 + aa, pw = c0 + bb;
           const int p = valid ? (int)__umul24((unsigned)ph, (unsigned)m.W) + pw : HW + lane;
           float lnew, rnew;
-          const float e = position_delta<MODEL, win, GL, RV>(m, xs, lg, lam, rv, p, aa, bb, ph, pw,
-                                                         P, amp_o, amp_n, ao_h, ao_w, an_h, an_w,
-                                                         lnew, rnew);
+          const float e = position_delta<MODEL, win, GL, RV, TB>(m, xs, lg, lam, rv, tab, tinv, p,
+                                                             aa, bb, ph, pw, P, amp_o, amp_n,
+                                                             ao_h, ao_w, an_h, an_w, lnew, rnew);
           acc1 = valid ? e : 0.f;
           s_lam[2 * np] = lnew;
           if constexpr (RV) s_rv[2 * np] = rnew;
@@ -743,8 +786,9 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           const int ph = r0 + aa, pw = c0 + bb;
           const int p = (int)__umul24((unsigned)ph, (unsigned)m.W) + pw;
           float lnew, rnew;
-          acc += position_delta<MODEL, true, GL, RV>(m, xs, lg, lam, rv, p, aa, bb, ph, pw, P, amp_o,
-                                                     amp_n, ao_h, ao_w, an_h, an_w, lnew, rnew);
+          acc += position_delta<MODEL, true, GL, RV, TB>(m, xs, lg, lam, rv, tab, tinv, p, aa, bb,
+                                                         ph, pw, P, amp_o, amp_n, ao_h, ao_w, an_h,
+                                                         an_w, lnew, rnew);
           if constexpr (decltype(WRITE)::value) {
             lam[p] = lnew;
             if constexpr (RV) rv[p] = rnew;
@@ -917,7 +961,9 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   if (lane == 0) {
     const int nw = min(kMhWaves, N - (int)blockIdx.x * kMhWaves);
     if (accept && a.K > 0) atomicAdd(&wg_acc, 1);
-    if constexpr (!TAIL) __threadfence_block();
+    // orders this wave's wg_acc add before its wg_done ticket (both builds;
+    // the TAIL build's agent-scope fence above precedes both atomics)
+    __threadfence_block();
     if (atomicAdd(&wg_done, 1) == nw - 1) {
       int32_t* cnt = a.acc_count + t;
       int32_t* ticket = a.acc_count + a.T + t;
@@ -968,30 +1014,56 @@ static int launch_mh1(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
   constexpr bool kTail = !FULL && PPL != 1;
   const bool tail = kTail && paired && a.has_tail;
   if (a.has_tail && !tail) return set_error(SMCDET_EINVAL, "fused step: unsupported shape");
+  // The LDS-cached variants, richest first, where their workgroups per CU
+  // (the occupancy the instantiation is built for) still fit the 160 KiB:
+  // PC (small tiles) = the per-wave PSF cache, RV (M71, 65..1024 px) = the
+  // per-wave 1/v image, TB = the radial PSF table (a.psf_tab set by the host
+  // for M71 models whose table passes its accuracy check).
+  auto fits = [&](size_t bytes, int wg_per_cu) {
+    return (size_t)wg_per_cu * (bytes + 1024) <= 160 * 1024;
+  };
+  auto with_tab = [&](size_t bytes) {
+    return ((bytes + 15) & ~(size_t)15) + (size_t)kTabNodes * sizeof(float4);
+  };
+  auto go_variant = [&](auto kern, size_t bytes) -> int {
+    int rc = ensure_lds((const void*)kern, bytes);
+    if (rc) return rc;
+    launch_sweep(kern, grid, dim3(kMhBlock), bytes, st, a);
+    return SMCDET_OK;
+  };
+  const bool tb = a.psf_tab != nullptr && paired && !tail;
   if constexpr (PPL == 1 && !FULL) {
-    // small tiles: the PSF cache (S rows of H*W floats per wave) where the
-    // SMCDET_SMALL_TILE_WAVES workgroups per CU still fit the 160 KiB LDS
+    // small tiles: the PSF cache (S rows of H*W floats per wave)
     const size_t lds_pc = lds + (size_t)kMhWaves * a.S * a.m.H * a.m.W * sizeof(float);
-    if (paired && !a.no_psf_cache &&
-        (size_t)SMCDET_SMALL_TILE_WAVES * (lds_pc + 1024) <= 160 * 1024) {
-      auto kpc = mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, true>;
-      int rc = ensure_lds((const void*)kpc, lds_pc);
-      if (rc) return rc;
-      launch_sweep(kpc, grid, dim3(kMhBlock), lds_pc, st, a);
-      return SMCDET_OK;
+    constexpr int wg = SMCDET_SMALL_TILE_WAVES;
+    if constexpr (MODEL == SMCDET_MODEL_M71) {
+      if (tb && !a.no_psf_cache && fits(with_tab(lds_pc), wg))
+        return go_variant(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, true,
+                                          false, true>, with_tab(lds_pc));
+    }
+    if (paired && !a.no_psf_cache && fits(lds_pc, wg))
+      return go_variant(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, true>,
+                        lds_pc);
+    if constexpr (MODEL == SMCDET_MODEL_M71) {
+      if (tb && fits(with_tab(lds), wg))
+        return go_variant(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, false,
+                                          false, true>, with_tab(lds));
     }
   }
   if constexpr (MODEL == SMCDET_MODEL_M71 && PPL > 1 && !FULL) {
-    // M71 register-render tiles: the 1/v image (HWp floats per wave) where
-    // the 4 workgroups per CU of the 4-waves-per-SIMD sweep still fit LDS
+    // M71 register-render tiles: the 1/v image (HWp floats per wave) and / or
+    // the PSF table, at 4 workgroups per CU (4 waves per SIMD)
     const size_t lds_rv = lds + (size_t)kMhWaves * (a.m.H * a.m.W + kWave) * sizeof(float);
-    if (paired && !tail && !a.no_rcp_cache && 4 * (lds_rv + 1024) <= 160 * 1024) {
-      auto krv = mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, false, true>;
-      int rc = ensure_lds((const void*)krv, lds_rv);
-      if (rc) return rc;
-      launch_sweep(krv, grid, dim3(kMhBlock), lds_rv, st, a);
-      return SMCDET_OK;
-    }
+    const bool rv = paired && !tail && !a.no_rcp_cache;
+    if (tb && rv && fits(with_tab(lds_rv), 4))
+      return go_variant(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, false, true,
+                                        true>, with_tab(lds_rv));
+    if (tb && fits(with_tab(lds), 4))
+      return go_variant(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, false,
+                                        false, true>, with_tab(lds));
+    if (rv && fits(lds_rv, 4))
+      return go_variant(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, false, true>,
+                        lds_rv);
   }
   const void* fn = tail     ?(const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, kTail>
                    : paired ? (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, false>
@@ -1066,6 +1138,139 @@ static bool tail_fusable(const smcdet_image_model_t& m, int N, int S, uint32_t f
   // 4 waves per SIMD = 4 workgroups per CU must still fit the 160 KiB LDS
   return 4 * (need + 2048) <= 160 * 1024;
 }
+
+// ---- the radial PSF table (psf_tab, device.h) --------------------------------
+// Device copies live in a module-scope table of slots, one per (device, PSF
+// parameters); a slot is filled once (upload + stream synchronisation, so any
+// later launch on any stream sees it) and reused by every later sweep.
+namespace smcdet {
+constexpr int kTabSlots = 8;
+__device__ float4 g_psf_tab[kTabSlots][kTabNodes];
+
+struct TabEntry {
+  int dev, slot;
+  float key[8];
+  float inv_h;
+};
+static std::mutex g_tab_mu;
+static std::vector<TabEntry> g_tab_entries;
+
+// psi(r^2) of psf_raw (device.h) for the float32 model constants, in double
+static double psf_raw_d(const DevModel& m, double x) {
+  return exp2((double)m.k1 * x) + (double)m.b * exp2((double)m.k2 * x) +
+         (double)m.p0 * exp2((double)m.kb * log2(1.0 + (double)m.k3 * x));
+}
+
+// The cubic per node (least squares at 16 Chebyshev points of t in [-1/2,
+// 1/2]; node 0 only [0, 1/2]) over r^2 in [0, 2(R + 3/2)^2]: every position of
+// a window (|dh|, |dw| <= R + 1/2) and of a union window of anchors one pixel
+// apart.  Returns false when the fit's relative error exceeds 2e-7 anywhere
+// (an unusually sharp profile or a large radius): the sweep then keeps the
+// exp2/log2 form, whose float32 evaluation errs by up to 7.5e-7.  (M71 at
+// R = 8: fit error 1.1e-7 at r^2 = 0.53, about half an ulp of the core value;
+// 3.0e-7 with the float32 coefficients and Horner steps.)
+static bool psf_table_build(const DevModel& m, float4* tab, float* inv_h_out) {
+  const double xmax = 2.0 * (m.R + 1.5) * (m.R + 1.5);
+  const float inv_h = (float)(kTabIntervals / xmax);
+  const double h = 1.0 / (double)inv_h;  // the spacing the device's index implies
+  constexpr int kPts = 16;
+  double worst = 0.0;
+  for (int i = 0; i < kTabNodes; ++i) {
+    double ata[4][5] = {};
+    for (int k = 0; k < kPts; ++k) {
+      const double c = 0.5 * cos((2.0 * k + 1.0) / (2.0 * kPts) * M_PI);
+      const double t = i == 0 ? 0.5 * (c + 0.5) : c;
+      const double y = psf_raw_d(m, (i + t) * h);
+      const double v[4] = {1.0, t, t * t, t * t * t};
+      for (int r = 0; r < 4; ++r) {
+        for (int q = 0; q < 4; ++q) ata[r][q] += v[r] * v[q];
+        ata[r][4] += v[r] * y;
+      }
+    }
+    for (int c = 0; c < 4; ++c) {  // Gauss-Jordan on the 4x4 normal equations
+      int piv = c;
+      for (int r = c + 1; r < 4; ++r)
+        if (fabs(ata[r][c]) > fabs(ata[piv][c])) piv = r;
+      for (int q = 0; q < 5; ++q) std::swap(ata[c][q], ata[piv][q]);
+      for (int r = 0; r < 4; ++r) {
+        if (r == c) continue;
+        const double f = ata[r][c] / ata[c][c];
+        for (int q = c; q < 5; ++q) ata[r][q] -= f * ata[c][q];
+      }
+    }
+    double co[4];
+    for (int r = 0; r < 4; ++r) co[r] = ata[r][4] / ata[r][r];
+    if (!(std::isfinite(co[0]) && std::isfinite(co[1]) && std::isfinite(co[2]) &&
+          std::isfinite(co[3])))
+      return false;
+    for (int k = 0; k <= 8; ++k) {  // the fit's own error (double), node interval
+      const double t = i == 0 ? 0.0625 * k : -0.5 + 0.125 * k;
+      const double y = psf_raw_d(m, (i + t) * h);
+      const double pv = co[0] + t * (co[1] + t * (co[2] + t * co[3]));
+      if (y > 0) worst = fmax(worst, fabs(pv - y) / y);
+    }
+    tab[i] = make_float4((float)co[0], (float)co[1], (float)co[2], (float)co[3]);
+  }
+  *inv_h_out = inv_h;
+  return worst <= 2e-7;
+}
+
+// the device table for this model (null: not applicable -> exp2/log2 form)
+static int psf_table_device(const smcdet_image_model_t& mdl, const DevModel& m, hipStream_t st,
+                            const float4** out, float* inv_h) {
+  *out = nullptr;
+  if (mdl.model != SMCDET_MODEL_M71) return SMCDET_OK;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return set_error(SMCDET_EHIP, "hipGetDevice failed");
+  const float key[8] = {m.k1, m.k2, m.k3, m.kb, m.b, m.p0, (float)m.R, 0.f};
+  std::lock_guard<std::mutex> lock(g_tab_mu);
+  void* base = nullptr;
+  if (hipGetSymbolAddress(&base, HIP_SYMBOL(g_psf_tab)) != hipSuccess)
+    return set_error(SMCDET_EHIP, "hipGetSymbolAddress(g_psf_tab) failed");
+  int used = 0;
+  for (const TabEntry& e : g_tab_entries) {
+    if (e.dev != dev) continue;
+    ++used;
+    if (memcmp(e.key, key, sizeof(key)) == 0) {
+      if (e.slot < 0) return SMCDET_OK;  // known not to meet the accuracy bound
+      *out = reinterpret_cast<const float4*>(base) + (size_t)e.slot * kTabNodes;
+      *inv_h = e.inv_h;
+      return SMCDET_OK;
+    }
+  }
+  std::vector<float4> host(kTabNodes);
+  TabEntry e{};
+  e.dev = dev;
+  memcpy(e.key, key, sizeof(key));
+  if (!psf_table_build(m, host.data(), &e.inv_h)) {
+    e.slot = -1;
+    g_tab_entries.push_back(e);
+    return SMCDET_OK;
+  }
+  int slots = 0;
+  for (const TabEntry& x : g_tab_entries) slots += (x.dev == dev && x.slot >= 0);
+  if (slots >= kTabSlots) {
+    // every slot taken: wait for the device, then start over with this one
+    if (hipDeviceSynchronize() != hipSuccess) return set_error(SMCDET_EHIP, "sync failed");
+    std::vector<TabEntry> keep;
+    for (const TabEntry& x : g_tab_entries)
+      if (x.dev != dev) keep.push_back(x);
+    g_tab_entries.swap(keep);
+    slots = 0;
+  }
+  (void)used;
+  e.slot = slots;
+  if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_psf_tab), host.data(), kTabNodes * sizeof(float4),
+                             (size_t)e.slot * kTabNodes * sizeof(float4), hipMemcpyHostToDevice,
+                             st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return set_error(SMCDET_EHIP, "PSF table upload failed");
+  g_tab_entries.push_back(e);
+  *out = reinterpret_cast<const float4*>(base) + (size_t)e.slot * kTabNodes;
+  *inv_h = e.inv_h;
+  return SMCDET_OK;
+}
+}  // namespace smcdet
 
 static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t* prior,
                          const smcdet_mh_t* mh, const float* tiled_image,
@@ -1205,6 +1410,11 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
   a.skip_done = (flags & SMCDET_MH_SKIP_DONE) != 0;
   a.no_psf_cache = (flags & SMCDET_MH_NO_PSF_CACHE) != 0;
   a.no_rcp_cache = (flags & SMCDET_MH_NO_RCP_CACHE) != 0;
+  if (a.m.model == SMCDET_MODEL_M71 && !full && !global_tile && !a.scalar_slots &&
+      !(flags & SMCDET_MH_NO_PSF_TABLE)) {
+    rc = psf_table_device(*model, a.m, st, &a.psf_tab, &a.tab_inv_h);
+    if (rc) return rc;
+  }
   rc = a.m.model == SMCDET_MODEL_M71
            ? launch_mh<SMCDET_MODEL_M71>(a, replay != nullptr, full, grid, lds, st)
            : launch_mh<SMCDET_MODEL_POISSON>(a, replay != nullptr, full, grid, lds, st);

@@ -128,6 +128,32 @@ __device__ __forceinline__ double vblock_sumd(const double (&a)[VLayout<NT>::VPT
   return sa;
 }
 template <int NT>
+__device__ __forceinline__ void vblock_sum2d(const double (&a)[VLayout<NT>::VPT],
+                                             const double (&b)[VLayout<NT>::VPT], double& A,
+                                             double& B, TileRed* r, int& parity) {
+  const int lane = threadIdx.x & 63;
+  const int k = parity;
+  parity ^= 1;
+#pragma unroll
+  for (int h = 0; h < VLayout<NT>::VPT; ++h) {
+    const double x = wave_sum(a[h]);
+    const double y = wave_sum(b[h]);
+    if (lane == 0) {
+      r->d[k][vwave<NT>(h)][0] = x;
+      r->d[k][vwave<NT>(h)][1] = y;
+    }
+  }
+  __syncthreads();
+  double sa = 0.0, sb = 0.0;
+#pragma unroll
+  for (int i = 0; i < kTW; ++i) {
+    sa += r->d[k][i][0];
+    sb += r->d[k][i][1];
+  }
+  A = sa;
+  B = sb;
+}
+template <int NT>
 __device__ __forceinline__ void vblock_sum2f(const float (&a)[VLayout<NT>::VPT],
                                              const float (&b)[VLayout<NT>::VPT], float& A,
                                              float& B, TileRed* r, int& parity) {
@@ -356,6 +382,7 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
 
   // ------------------------------------------------------------------ temper
   float d_new = 0.f;  // float32 temperature increment, when tempered here
+  float lm_t = -INFINITY;  // the temper pass's max log-likelihood
   if (a.flags & kDoTemper) {
     const float tau = a.temperature[t];
     float lmv[VPT];
@@ -367,6 +394,7 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
         if (ll.valid(h, j, N)) lmv[h] = fmaxf(lmv[h], ll.l[h][j]);
     }
     const float lm = vblock_max<NT>(lmv, &red, parity);
+    lm_t = lm;
     SMC_TRACE(trow, 1);
     const double thr = a.ess_threshold;
     auto f = [&](double x) { return block_ess_objective(ll, N, lm, x, thr, &red, parity); };
@@ -406,38 +434,44 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
         }
       }
     }
-    const float mx = vblock_max<NT>(mxv, &red, parity);
-    double ssum[VPT];
+    // max of the weights' exponents: tempered here with a finite max
+    // log-likelihood, it is fl(d * lmax) (d >= 0: rounding and nan_to_num
+    // are monotone, the block_ess_objective argument), no reduction
+    const float mt = d * lm_t;
+    const float mx = ((a.flags & kDoTemper) && isfinite(mt)) ? mt
+                                                            : vblock_max<NT>(mxv, &red, parity);
+    double ssum[VPT], qsum[VPT];
 #pragma unroll
     for (int h = 0; h < VPT; ++h) {
-      double s[PER];
+      double s[PER], q[PER];
 #pragma unroll
       for (int j = 0; j < PER; ++j) {
         e[h][j] = ll.valid(h, j, N) ? expf(e[h][j] - mx) : 0.f;
         s[j] = (double)e[h][j];
+        q[j] = s[j] * s[j];
       }
       ssum[h] = tree_sum(s);
+      qsum[h] = tree_sum(q);
     }
-    const float sf = (float)vblock_sumd<NT>(ssum, &red, parity);
-    double qsum[VPT];
+    // one reduction for the sum and the sum of squares: ESS = 1 / sum W^2
+    // = (sum e)^2 / sum e^2 (sampler.py:187-190), in double
+    double se, qe;
+    vblock_sum2d<NT>(ssum, qsum, se, qe, &red, parity);
+    const float sf = (float)se;
 #pragma unroll
     for (int h = 0; h < VPT; ++h) {
-      double q[PER];
 #pragma unroll
       for (int j = 0; j < PER; ++j) {
         const float wv = e[h][j] / sf;
-        q[j] = (double)wv * (double)wv;
         if (ll.valid(h, j, N)) {
           wg[vthread<NT>(h) + j * kTB] = wv;
           buf[vthread<NT>(h) + j * kTB] = wv;
         }
       }
-      qsum[h] = tree_sum(q);
     }
-    const double qs = vblock_sumd<NT>(qsum, &red, parity);
     SMC_TRACE(trow, 4);
     if (threadIdx.x == 0) {
-      a.ess[t] = (float)(1.0 / qs);
+      a.ess[t] = (float)(se * se / qe);
       a.logZ[t] = (a.logZ[t] + mx) + logf(sf / (float)N);
     }
   }
@@ -527,99 +561,43 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
     int64_t* idxg = a.idx + (size_t)t * N;
     if (a.method == SMCDET_RESAMPLE_SYSTEMATIC) {
       // bucketize(u, bins), u_n = (n + U) / N in float32 (sampler.py:144),
-      // right=False: idx[n] = #{i : bins[i] < u_n}.  With cnt(i) = #{n : u_n <= bins[i]}
-      // (monotone in i), idx[n] = #{i : cnt(i) <= n}: the last bin of every run of
-      // equal cnt writes i+1 to slot[cnt], and a prefix max over slots gives idx.
-      // Exact (u_n is recomputed with the same float ops) and load-balanced
-      // whatever the weight degeneracy, unlike a per-n search.
-      int* slot = reinterpret_cast<int*>(buf + N);  // N+1 ints
+      // right=False: idx[n] = #{i : bins[i] < u_n}, clamped to N - 1.  bins
+      // is monotone (float32 roundings of a running sum of non-negative
+      // weights), so the count is a binary search: binary lifting with
+      // power-of-two steps, log2(N) LDS reads per n whatever the weights'
+      // degeneracy, G searches per thread interleaved.  The test
+      // bins[i] < u_n is exact: u_n is formed with the reference's float
+      // ops, and for N a power of two the division is an exact scaling, so
+      // b < u_n  <=>  b*N < fl(n + U) (exact) without the division.
       const float Nf = (float)N;
-      auto un = [&](int n) { return ((float)n + U) / Nf; };
-      // For N a power of two the division is an exact scaling:
-      // u_n <= b  <=>  fl(n + U) <= b*N (exact), and n <= fl(n + U) <= n + 1,
-      // so every n < floor(b*N) counts and only n = floor(b*N) needs a test.
       const bool pow2 = (N & (N - 1)) == 0;
-      auto cnt = [&](float b) {
-        if (pow2) {
-          const float B = b * Nf;
-          int c = (int)fminf(fmaxf(floorf(B), 0.f), Nf);
-          c += (c < N && (float)c + U <= B) ? 1 : 0;
-          return c;
+      int top = 1;
+      while (2 * top <= N) top *= 2;
+      constexpr int G = 8;
+      for (int base = threadIdx.x; base < N; base += NT * G) {
+        float key[G];
+        int lo[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const float nu = (float)(base + g * NT) + U;
+          key[g] = pow2 ? nu : nu / Nf;
+          lo[g] = 0;
         }
-        int c = (int)fminf(fmaxf(floorf(b * Nf - U), 0.f), Nf);
-        while (c > 0 && un(c - 1) > b) --c;
-        while (c < N && un(c) <= b) ++c;
-        return c;
-      };
-      for (int i = threadIdx.x; i <= N; i += NT) slot[i] = 0;
-      __syncthreads();
-      SMC_TRACE(trow, 6);
-      for (int i = threadIdx.x; i < N; i += NT) {
-        const int ci = cnt(buf[i]);
-        const int cnext = (i + 1 < N) ? cnt(buf[i + 1]) : -1;
-        if (cnext != ci) slot[ci] = i + 1;
-      }
-      __syncthreads();
-      SMC_TRACE(trow, 7);
-      // prefix max over slot[0..N-1], contiguous chunk per virtual thread
-      int sv[VPT][8];
-      int incl_m[VPT];
+        for (int step = top; step > 0; step >>= 1) {
 #pragma unroll
-      for (int h = 0; h < VPT; ++h) {
-        int pm = 0;
-        if (vec8) {
-          if (b0[h] < b1[h]) {
-            const int4 v0 = *reinterpret_cast<const int4*>(slot + b0[h]);
-            const int4 v1 = *reinterpret_cast<const int4*>(slot + b0[h] + 4);
-            sv[h][0] = v0.x; sv[h][1] = v0.y; sv[h][2] = v0.z; sv[h][3] = v0.w;
-            sv[h][4] = v1.x; sv[h][5] = v1.y; sv[h][6] = v1.z; sv[h][7] = v1.w;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) pm = max(pm, sv[h][i]);
-          }
-        } else {
-          for (int i = b0[h]; i < b1[h]; ++i) pm = max(pm, slot[i]);
-        }
-        incl_m[h] = pm;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int y = __shfl_up(incl_m[h], o, kWave);
-          if (lane >= o) incl_m[h] = max(incl_m[h], y);
-        }
-      }
-      const int k2 = parity;
-      parity ^= 1;
-#pragma unroll
-      for (int h = 0; h < VPT; ++h)
-        if (lane == 63) red.i[k2][vwave<NT>(h)] = incl_m[h];
-      __syncthreads();
-#pragma unroll
-      for (int h = 0; h < VPT; ++h) {
-        int run_m = __shfl_up(incl_m[h], 1, kWave);
-        if (lane == 0) run_m = 0;
-        for (int i = 0; i < vwave<NT>(h); ++i) run_m = max(run_m, red.i[k2][i]);
-        // in place: slot[i] becomes idx[i] (each virtual thread owns its chunk)
-        if (vec8) {
-          if (b0[h] < b1[h]) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              run_m = max(run_m, sv[h][i]);
-              sv[h][i] = min(run_m, N - 1);
-            }
-            *reinterpret_cast<int4*>(slot + b0[h]) =
-                make_int4(sv[h][0], sv[h][1], sv[h][2], sv[h][3]);
-            *reinterpret_cast<int4*>(slot + b0[h] + 4) =
-                make_int4(sv[h][4], sv[h][5], sv[h][6], sv[h][7]);
-          }
-        } else {
-          for (int i = b0[h]; i < b1[h]; ++i) {
-            run_m = max(run_m, slot[i]);
-            slot[i] = min(run_m, N - 1);
+          for (int g = 0; g < G; ++g) {
+            const int i = lo[g] + step - 1;
+            const float b = buf[min(i, N - 1)];
+            const bool less = pow2 ? (b * Nf < key[g]) : (b < key[g]);
+            lo[g] += (i < N && less) ? step : 0;
           }
         }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int n = base + g * NT;
+          if (n < N) idxg[n] = (int64_t)min(lo[g], N - 1);
+        }
       }
-      __syncthreads();
-      SMC_TRACE(trow, 8);
-      for (int n = threadIdx.x; n < N; n += NT) idxg[n] = (int64_t)slot[n];
       SMC_TRACE(trow, 9);
     } else {
       // multinomial (sampler.py:127-140): target = u * total, first bin > target

@@ -1155,6 +1155,15 @@ def gen_stats(which, seeds, part=None):
         mk = lambda: SingleComponentMH(K, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])  # noqa
         model, tile, N, method = m71_model(32), 32, 4096, "systematic"
         max_iters = 1000
+    elif which == "c4":
+        # BASELINE configs[3]: an 8x8 M71 cutout at the real
+        # source density (the "m71" image: generate_images with M71Prior(0, 100),
+        # experiments/m71synthetic/generate_images.py:27-67), S=10, N=4096, K=100
+        res = m71_truth_image(8, 0)
+        img = res[-1][0]
+        pr = m71_prior(8, 10, 10)
+        mk = lambda: SingleComponentMH(100, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])  # noqa
+        model, tile, N, method = m71_model(8), 8, 4096, "systematic"
     elif which == "c2_reduced":
         # the headline geometry (one 32x32 M71 tile, S=10,
         # counts_rate 5/40^2 truth with <= 10 sources) at reduced N and K
@@ -1194,14 +1203,16 @@ def gen_stats(which, seeds, part=None):
                              s.posterior_mean_total_flux(s.pruned_fluxes).flatten()[0]),
                          runtime_s=dt))
         print(which, seed, rows[-1]["logZ"], rows[-1]["iters"], f"{dt:.1f}s", flush=True)
-    cfg = dict(which=which, tile=tile, N=N, S=pr.max_objects, K=mk().num_iters, method=method,
-               counts_rate=float(pr.counts_rate) if hasattr(pr, "counts_rate") else None,
-               rho=0.5, torch_threads=torch.get_num_threads(), max_smc_iters=max_iters,
-               kernel="mala" if which.endswith("mala") else "mh")
-    path = os.path.join(HERE, f"stats_{which}.json" if part is None
-                        else f"stats_{which}.part{part}.json")
-    with open(path, "w") as f:
-        json.dump(dict(config=cfg, image=img.numpy().tolist(), runs=rows), f)
+        # written after every seed: long background runs keep what they finished
+        cfg = dict(which=which, tile=tile, N=N, S=pr.max_objects, K=mk().num_iters,
+                   method=method,
+                   counts_rate=float(pr.counts_rate) if hasattr(pr, "counts_rate") else None,
+                   rho=0.5, torch_threads=torch.get_num_threads(), max_smc_iters=max_iters,
+                   kernel="mala" if which.endswith("mala") else "mh")
+        path = os.path.join(HERE, f"stats_{which}.json" if part is None
+                            else f"stats_{which}.part{part}.json")
+        with open(path, "w") as f:
+            json.dump(dict(config=cfg, image=img.numpy().tolist(), runs=rows), f)
     print("wrote", path)
 
 
@@ -1224,7 +1235,7 @@ def cssmc_truth_image():
     return m71_model(8).sample(l, f)[0, 0, :, :, 0]
 
 
-def gen_cssmc(seeds, smax=4, N=512, K=50):
+def gen_cssmc(seeds, smax=4, N=512, K=50, which="cssmc", part=None):
     """CS-SMC targets (manuscript.tex:314-356): for each count s, the
     reference's fixed-count SMCsampler (M71Prior with min = max = s) over many
     seeds -> log Z_s; log Z_0 = the reference's log-likelihood of the empty
@@ -1232,8 +1243,11 @@ def gen_cssmc(seeds, smax=4, N=512, K=50):
     Poisson count prior; p(s|x) from each seed's log Z vector."""
     import contextlib
     import io
-    torch.set_num_threads(8)
-    img = cssmc_truth_image()
+    torch.set_num_threads(int(os.environ.get("GOLDEN_THREADS", "8")))
+    # "c5": BASELINE configs[4] (SURVEY §8d C5): the C4 cutout (the "m71"
+    # image) with count strata 0..6 at N=8192 per count, K=100
+    # (manuscript.tex:566,648)
+    img = cssmc_truth_image() if which == "cssmc" else m71_truth_image(8, 0)[-1][0]
     model = m71_model(8)
     ll0 = float(model.loglikelihood(img.reshape(1, 1, 8, 8), torch.full((1, 1, 1, 1, 2), 4.0),
                                     torch.zeros(1, 1, 1, 1)).flatten()[0])
@@ -1254,12 +1268,13 @@ def gen_cssmc(seeds, smax=4, N=512, K=50):
         v = np.array(lz) + log_ps
         p = np.exp(v - v.max())
         rows.append(dict(seed=seed, logZ=lz, iters=iters, count_posterior=(p / p.sum()).tolist()))
-        print("cssmc", seed, np.round(lz, 2).tolist(), flush=True)
-    cfg = dict(tile=8, N=N, K=K, smin=0, smax=smax, method="systematic", rho=0.5, pad=4,
-               log_count_prior=log_ps.tolist(), loglik_empty=ll0)
-    path = os.path.join(HERE, "stats_cssmc.json")
-    with open(path, "w") as f:
-        json.dump(dict(config=cfg, image=img.numpy().tolist(), runs=rows), f)
+        print(which, seed, np.round(lz, 2).tolist(), iters, flush=True)
+        cfg = dict(tile=8, N=N, K=K, smin=0, smax=smax, method="systematic", rho=0.5, pad=4,
+                   log_count_prior=log_ps.tolist(), loglik_empty=ll0)
+        path = os.path.join(HERE, f"stats_{which}.json" if part is None
+                            else f"stats_{which}.part{part}.json")
+        with open(path, "w") as f:
+            json.dump(dict(config=cfg, image=img.numpy().tolist(), runs=rows), f)
     print("wrote", path)
 
 
@@ -1417,6 +1432,12 @@ if __name__ == "__main__":
     elif what == "cssmc":
         n = int(sys.argv[2]) if len(sys.argv) > 2 else 16
         gen_cssmc(list(range(n)))
+    elif what == "c5":
+        # c5 [n] [first]: count-stratified reference runs on the C4 cutout
+        n = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+        first = int(sys.argv[3]) if len(sys.argv) > 3 else None
+        gen_cssmc(list(range(first or 0, (first or 0) + n)), smax=6, N=8192, K=100, which="c5",
+                  part=first)
     elif what == "stats":
         # stats <which> [n] [first]: seeds first..first+n-1; with `first` the
         # rows go to stats_<which>.part<first>.json (parallel partial runs),

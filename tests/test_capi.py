@@ -66,13 +66,13 @@ def test_invalid_arguments_fail_loudly_without_gpu():
     assert b"null" in L.smcdet_last_error()
     m = _hip.ImageModelC()
     m.model, m.H, m.W, m.psf_radius = 1, 300, 300, 8  # 90,000 px > 65,536
-    rc = L.smcdet_loglik(ctypes.byref(m), ctypes.c_void_p(1), ctypes.c_void_p(1),
-                         ctypes.c_void_p(1), 1, 1, 1, ctypes.c_void_p(1), None)
+    rc = L.smcdet_loglik(ctypes.byref(m), ctypes.c_void_p(1), ctypes.c_void_p(2),
+                         ctypes.c_void_p(3), 1, 1, 1, ctypes.c_void_p(4), None)
     assert rc == -2
     # above 4,096 px only the M71 model has the global-memory paths
     m.model, m.H, m.W = 2, 100, 100
-    rc = L.smcdet_loglik(ctypes.byref(m), ctypes.c_void_p(1), ctypes.c_void_p(1),
-                         ctypes.c_void_p(1), 1, 1, 1, ctypes.c_void_p(1), None)
+    rc = L.smcdet_loglik(ctypes.byref(m), ctypes.c_void_p(1), ctypes.c_void_p(2),
+                         ctypes.c_void_p(3), 1, 1, 1, ctypes.c_void_p(4), None)
     assert rc == -2 and b"M71" in L.smcdet_last_error()
     # the LDS-resident kernels (MALA, MCMC chains, aggregation) keep 4,096 px
     m.model = 1
@@ -108,3 +108,48 @@ def test_launch_timing_pool_without_gpu():
     assert L.smcdet_launch_timing(-1) == -1
     assert L.smcdet_launch_timing(0) == 0
     assert _hip.launch_timing_read(4) == []
+
+
+def test_alias_check_rejects_shared_output_pointer():
+    """an output pointer equal to another argument's (a
+    freed temporary reused by the caching allocator) is rejected before the
+    launch; the header's in-place pairs pass."""
+    import ctypes
+
+    import pytest
+
+    from smcdet_amd import _hip
+    P = ctypes.c_void_p
+    # smcdet_resample_index(weights, T, N, method, seed, offset, u, idx, stream)
+    ok = (P(0x1000), 1, 8, 1, 0, 0, None, P(0x2000), P(0x9))
+    _hip.check_aliases("smcdet_resample_index", ok)
+    bad = (P(0x1000), 1, 8, 1, 0, 0, P(0x2000), P(0x2000), P(0x9))
+    with pytest.raises(ValueError, match="argument 7"):
+        _hip.check_aliases("smcdet_resample_index", bad)
+    # the stream is not compared
+    _hip.check_aliases("smcdet_resample_index", (P(0x1000), 1, 8, 1, 0, 0, None, P(0x2000),
+                                                 P(0x2000)))
+    # MH sweep: locs_in == locs_out (no ancestor gather) is the header's in-place form
+    args = [None] * 27
+    args[10] = args[13] = P(0x3000)
+    args[21] = P(0x4000)
+    _hip.check_aliases("smcdet_mh_sweep", tuple(args))
+    args[22] = P(0x4000)  # acc_rate aliasing loglik_out
+    with pytest.raises(ValueError):
+        _hip.check_aliases("smcdet_mh_sweep", tuple(args))
+
+
+def test_ptr_keeps_temporaries_alive():
+    import gc
+
+    import torch
+
+    from smcdet_amd import _hip
+    t = torch.empty(4)
+    addr = t.data_ptr()
+    import weakref
+    r = weakref.ref(t)
+    p = _hip.ptr(t)
+    del t
+    gc.collect()
+    assert r() is not None and p.value == addr

@@ -134,3 +134,70 @@ def test_aggregate_to_128x128_image():
     assert c.max() <= 48
     det = float(agg.pruned_counts.float().mean())
     assert 7.0 <= det <= 12.0, det
+
+
+def test_poisson_64x64_joint_tile_reduced_waves_vs_oracle():
+    """The basic (Poisson) image model has no global-memory sweep: a 64x64
+    joint tile (image + lgamma(x+1), and per wave two rate images and the
+    catalog: 160 KiB at 4 waves is exceeded for any S) runs the LDS sweep at
+    the largest wave count that fits, no workspace.  l_p, l_c and
+    a replayed sweep on the bridging target against the oracle.  Tolerance
+    rtol 1e-5: a 4,096-pixel Poisson sum carries the float32 lgamma(x + 1)
+    roundings (the reference's own float32 Poisson.log_prob does too) --
+    ~0.2 nats, the same for every particle, against the float64 oracle."""
+    from smcdet_amd import _hip
+    from smcdet_amd.aggregate import aggregate_sweep
+    from smcdet_amd.images import ImageModel
+    from smcdet_amd.prior import ParetoStarPrior
+    from tests._params import BASIC_BACKGROUND, BASIC_FLUX_ALPHA, BASIC_FLUX_SCALE, BASIC_PSF_STDEV
+    H = W = 64
+    S, N, K, axis = 8, 24, 10, 0
+    model = ImageModel(image_height=H, image_width=W, psf_radius=8, psf_stdev=BASIC_PSF_STDEV,
+                       background=BASIC_BACKGROUND)
+    prior = ParetoStarPrior(min_objects=0, max_objects=S, image_height=H, image_width=W,
+                            flux_scale=BASIC_FLUX_SCALE * 0.9, flux_alpha=BASIC_FLUX_ALPHA, pad=2)
+    om = O.BasicModel(H, W, BASIC_BACKGROUND, 8, BASIC_PSF_STDEV)
+    op = O.ParetoPriorP(0, S, H, W, 2, BASIC_FLUX_SCALE * 0.9, BASIC_FLUX_ALPHA)
+    from smcdet_amd.kernel import SingleComponentMH
+    k = SingleComponentMH(K, 0.1, 100.0, BASIC_FLUX_SCALE * 0.9, 1e6)
+    k.locs_min, k.locs_max = prior.loc_prior.low, prior.loc_prior.high
+    assert _hip.lib().smcdet_aggregate_workspace(_hip.ref(model._cmodel()), 1, N, S) == 0
+    rng = np.random.default_rng(41)
+    c = rng.integers(1, S + 1, (1, 1, N)).astype(np.float32)
+    mask = np.arange(S) < c[..., None]
+    l = np.stack([rng.uniform(-2, H + 2, (1, 1, N, S)), rng.uniform(-2, W + 2, (1, 1, N, S))],
+                 -1).astype(np.float32) * mask[..., None]
+    f = (rng.uniform(400, 3000, (1, 1, N, S)) * mask).astype(np.float32)
+    tl = np.stack([rng.uniform(6, H - 6, 5), rng.uniform(6, W - 6, 5)], -1).reshape(1, 1, 1, 5, 2)
+    tf = rng.uniform(800, 4000, 5).reshape(1, 1, 1, 5)
+    rate = O.render_rate(tl, tf, om)[0, 0, :, :, 0]
+    d = rng.poisson(rate).astype(np.float32)[None, None]
+    tau0 = D(np.full((1, 1), 0.3, np.float32))
+    _, lo, _, lp, lc, _ = aggregate_sweep(model, prior, k, axis, D(d), tau0, D(c), D(l), D(f),
+                                          num_iters=0)
+    np.testing.assert_array_equal(N_(lo), l)
+    olp, olc = A.parent_child_loglik(d, c, l, f, om, axis)
+    np.testing.assert_allclose(N_(lp), olp, rtol=1e-5, atol=3e-3)
+    np.testing.assert_allclose(N_(lc), olc, rtol=1e-5, atol=3e-3)
+    comp = np.minimum((rng.random((K,) + c.shape) * c).astype(np.int32), c.astype(np.int32) - 1)
+    uloc = rng.random((K,) + c.shape + (2,)).astype(np.float32)
+    uflux = rng.random((K,) + c.shape).astype(np.float32)
+    uacc = rng.random((K,) + c.shape).astype(np.float32)
+    tau = np.full((1, 1), 0.4, np.float32)
+    ol, of, oacc, marg = A.agg_mh_sweep(d, c, l, f, tau, op, om, axis,
+                                        O.MHParams(K, 0.1, 100.0, BASIC_FLUX_SCALE * 0.9, 1e6),
+                                        comp, uloc, uflux, uacc, trace=True)
+    rp = dict(comp=torch.as_tensor(comp.astype(np.int32)), uloc=torch.as_tensor(uloc),
+              uflux=torch.as_tensor(uflux), uacc=torch.as_tensor(uacc))
+    ws = torch.zeros(2, device=DEV, dtype=torch.int32)
+    co, lo, fo, lp, lc, acc = aggregate_sweep(model, prior, k, axis, D(d), D(tau), D(c), D(l),
+                                              D(f), replay=rp, acc_workspace=ws)
+    clear = np.all(np.abs(np.nan_to_num(marg, nan=0.0)) > 1e-3, axis=0)
+    assert clear.mean() > 0.7, clear.mean()
+    assert oacc.any() and (~oacc).any()
+    np.testing.assert_allclose(N_(lo)[clear], ol[clear], rtol=0, atol=5e-5)
+    np.testing.assert_allclose(N_(fo)[clear], of[clear], rtol=3e-5, atol=1e-3)
+    olp, olc = A.parent_child_loglik(d, c, ol, of, om, axis)
+    np.testing.assert_allclose(N_(lp)[clear], olp[clear], rtol=1e-5, atol=3e-3)
+    np.testing.assert_allclose(N_(lc)[clear], olc[clear], rtol=1e-5, atol=3e-3)
+    assert int(ws.abs().sum()) == 0

@@ -1,0 +1,219 @@
+"""BASELINE.json configs[3] and [4] at their configured sizes.
+
+C4: 8x8 M71 cutouts at the real source density (truth from M71Prior(0, 100)
+    with the M71 counts_rate, as experiments/m71synthetic/generate_images.py:
+    27-67), S = 10, N = 4096, K = 100, systematic, rho = 0.5 -- 42 cutouts per
+    GPU (the 332 M71 cutouts of manuscript.tex:562 over 8 GPUs) as one
+    BatchSMC, run to temperature 1.
+C5: the same cutouts under count-stratified SMC (manuscript.tex:314-356),
+    counts 0..6 at N = 8192 per count (manuscript.tex:566,648), K = 100.
+
+Per image: temperature 1, finite log Z, ESS = rho*N at every tempering step
+whose increment is >= 1e-3; the first images equal runs of a smaller batch
+bit for bit.  Against the reference (tests/golden/stats_c4.json /
+stats_c5.json, make_golden.py `stats c4` / `c5`: the reference's own
+SMCsampler / fixed-count samplers on the "m71" cutout): mean log Z (per count
+for C5) within 1% and 3 pooled SE, final ESS, SMC iterations and the
+pruned-count histogram (C4), p(s|x) (C5).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests._params import GOLDEN, M71, p_m71_mh, p_m71_model, p_m71_prior
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+H = 8
+B = 42
+
+
+def _load(name):
+    path = os.path.join(GOLDEN, name)
+    if not os.path.exists(path):
+        pytest.skip(f"{name} not generated")
+    with open(path) as f:
+        return json.load(f)
+
+
+def _m71_image():
+    """The reference's "m71" cutout (make_golden.py m71_truth_image(8, 0)),
+    the image of stats_m71.json / stats_c4.json / stats_c5.json."""
+    with open(os.path.join(GOLDEN, "stats_m71.json")) as f:
+        return torch.tensor(json.load(f)["image"], dtype=torch.float32, device=DEV)
+
+
+def cutouts(n, seed=2000):
+    """n 8x8 M71 cutouts: the reference's "m71" image first, then draws of the
+    truth prior M71Prior(0, 100) (flux above the detection threshold, pad 4)
+    through M71ImageModel.sample on the device."""
+    from smcdet_amd.prior import M71Prior
+    torch.manual_seed(seed)
+    truth = M71Prior(min_objects=0, max_objects=100, counts_rate=M71["counts_rate"],
+                     image_height=H, image_width=H, flux_alpha=M71["flux_alpha"],
+                     flux_lower=M71["flux_detection_threshold"], flux_upper=M71["flux_upper"],
+                     pad=4)
+    model = p_m71_model(H)
+    c, l, f = truth.sample(num_catalogs=n - 1, device=DEV)
+    imgs = model.sample(l, f)[0, 0].permute(2, 0, 1)
+    return torch.cat([_m71_image()[None], imgs], 0).contiguous()
+
+
+def _traced(s):
+    """Records (temperature, ESS) of every tile after each tempering step."""
+    trace = []
+    orig = s._temper_reweight
+
+    def tr(with_resample, orig=orig):
+        orig(with_resample)
+        trace.append((s.temperature.flatten().cpu().numpy().copy(),
+                      s.ess.flatten().cpu().numpy().copy()))
+
+    s._temper_reweight = tr
+    return trace
+
+
+def _check_ess_trace(trace, rho_n, tiles):
+    taus = np.stack([t for t, _ in trace])   # [steps, T]
+    ess = np.stack([e for _, e in trace])
+    prev = np.vstack([np.zeros((1, taus.shape[1])), taus[:-1]])
+    delta = taus - prev
+    # a tempering step of an active tile that did not reach 1 lands on rho*N
+    # (increments below 1e-3: brentq's xtol is not small against them)
+    active = (delta >= 1e-3) & (taus < 1.0)
+    for t in tiles:
+        np.testing.assert_allclose(ess[active[:, t], t], rho_n, rtol=0.01, err_msg=f"tile {t}")
+
+
+def _c4_batch(images, seed, stopping="independent"):
+    from smcdet_amd.batch import BatchSMC
+    prior, model, mh = p_m71_prior(H, 10, 10), p_m71_model(H), p_m71_mh(100)
+    return BatchSMC(images, prior, model, mh, 4096, 0.5, "systematic",
+                    M71["flux_detection_threshold"], 100, stopping=stopping, seed=seed,
+                    device=DEV)
+
+
+def test_c4_full_size_batch():
+    images = cutouts(B)
+    b = _c4_batch(images, 12345)
+    trace = _traced(b.sampler)
+    b.run()
+    r = b.results()
+    s = b.sampler
+    assert float(s.temperature.min()) == 1.0
+    lz = r["log_normalizing_constant"].cpu().numpy()
+    assert np.isfinite(lz).all()
+    assert (r["num_iters"].cpu().numpy() >= 1).all()
+    _check_ess_trace(trace, 0.5 * 4096, range(B))
+    assert r["counts"].shape == (B, 4096) and r["locs"].shape == (B, 4096, 10, 2)
+    # the first two images of the batch are a 2-image batch's, bit for bit
+    # (draws keyed by (seed, tile, particle); independent stopping)
+    b2 = _c4_batch(images[:2].contiguous(), 12345)
+    b2.run()
+    r2 = b2.results()
+    for k in ("log_normalizing_constant", "num_iters", "counts", "locs", "fluxes"):
+        assert torch.equal(r[k][:2].cpu(), r2[k].cpu()), k
+
+
+def _se(a, b):
+    return np.sqrt(np.var(a, ddof=1) / len(a) + np.var(b, ddof=1) / len(b))
+
+
+def test_c4_statistical_vs_reference():
+    ref = _load("stats_c4.json")
+    rr = ref["runs"]
+    if len(rr) < 20:
+        pytest.skip(f"stats_c4.json: {len(rr)} reference runs (< 20)")
+    cfg = ref["config"]
+    assert (cfg["tile"], cfg["N"], cfg["S"], cfg["K"]) == (8, 4096, 10, 100)
+    img = torch.tensor(ref["image"], dtype=torch.float32, device=DEV)
+    n = 64  # independent copies of the cutout in one batch: 64 single-image runs
+    b = _c4_batch(img[None].expand(n, H, H).contiguous(), 777)
+    b.run()
+    r = b.results()
+    lz = r["log_normalizing_constant"].cpu().double().numpy()
+    fe = r["ess"].cpu().double().numpy()
+    it = r["num_iters"].cpu().double().numpy()
+    lz_ref = np.array([x["logZ"] for x in rr])
+    fe_ref = np.array([x["final_ess"] for x in rr])
+    it_ref = np.array([x["iters"] for x in rr])
+    se = _se(lz, lz_ref)
+    print("C4 log Z", lz.mean(), "+-", se, "ref", lz_ref.mean(), "final ESS", fe.mean(),
+          fe_ref.mean(), "iters", it.mean(), it_ref.mean())
+    assert abs(lz.mean() - lz_ref.mean()) <= 3 * se, (lz.mean(), lz_ref.mean(), se)
+    assert abs(lz.mean() - lz_ref.mean()) <= 0.01 * abs(lz_ref.mean()), (lz.mean(),
+                                                                         lz_ref.mean())
+    assert abs(fe.mean() - fe_ref.mean()) <= 3 * _se(fe, fe_ref), (fe.mean(), fe_ref.mean())
+    assert abs(it.mean() - it_ref.mean()) <= max(3 * _se(it, it_ref), 0.5), (it.mean(),
+                                                                           it_ref.mean())
+    pc = r["pruned_counts"].cpu().numpy()
+    hist = np.stack([np.bincount(p, minlength=11)[:11] / p.size for p in pc])
+    h_ref = np.array([x["pruned_hist"] for x in rr])[:, :11]
+    se_b = np.sqrt(hist.var(0, ddof=1) / len(hist) + h_ref.var(0, ddof=1) / len(h_ref))
+    assert np.all(np.abs(hist.mean(0) - h_ref.mean(0)) <= 3 * se_b + 0.01), (
+        hist.mean(0).round(3), h_ref.mean(0).round(3))
+
+
+def _c5(images, seed, N=8192):
+    from smcdet_amd.cssmc import CountStratifiedSMC
+    return CountStratifiedSMC(images.reshape(1, -1, H, H), H, p_m71_prior(H, 0, 6),
+                              p_m71_model(H), p_m71_mh(100), N, 0.5, "systematic",
+                              M71["flux_detection_threshold"], 100, print_every=10 ** 9,
+                              seed=seed, device=DEV)
+
+
+def _loglik_empty(images):
+    model = p_m71_model(H)
+    n = images.shape[0]
+    locs = torch.full((1, n, 1, 1, 2), 4.0, device=DEV)
+    return model.loglikelihood(images.reshape(1, n, H, H), locs,
+                               torch.zeros(1, n, 1, 1, device=DEV))[0, :, 0]
+
+
+def test_c5_full_size_cssmc():
+    images = cutouts(B, seed=2001)
+    cs = _c5(images, 4242)
+    trace = _traced(cs.sampler)
+    cs.run()
+    assert float(cs.temperature.min()) == 1.0          # every stratum of every cutout
+    lz = cs.log_normalizing_constant_per_count[0]       # [B, 7]
+    assert torch.isfinite(lz).all()
+    torch.testing.assert_close(lz[:, 0], _loglik_empty(images), rtol=1e-5, atol=1e-3)
+    p = cs.count_posterior[0]
+    assert (p >= 0).all()
+    torch.testing.assert_close(p.sum(-1), torch.ones(B, device=DEV), rtol=1e-5, atol=1e-5)
+    # strata with s >= 1 temper on rho*N; count 0 has a constant likelihood
+    # (one step to temperature 1)
+    NS = 7
+    tiles = [b * NS + k for b in range(B) for k in range(1, NS)]
+    _check_ess_trace(trace, 0.5 * 8192, tiles)
+    # output catalogs come from the stratum of their count
+    k = (cs.sample_index[0] // 8192).cpu().numpy()
+    np.testing.assert_array_equal(cs.counts[0].cpu().numpy(), k.astype(np.float32))
+
+
+def test_c5_statistical_vs_reference():
+    ref = _load("stats_c5.json")
+    rr = ref["runs"]
+    if len(rr) < 8:
+        pytest.skip(f"stats_c5.json: {len(rr)} reference runs (< 8)")
+    cfg = ref["config"]
+    assert (cfg["N"], cfg["K"], cfg["smax"]) == (8192, 100, 6)
+    img = torch.tensor(ref["image"], dtype=torch.float32, device=DEV)
+    n = 24
+    cs = _c5(img[None].expand(n, H, H).contiguous(), 99)
+    cs.run()
+    lz = cs.log_normalizing_constant_per_count[0].double().cpu().numpy()   # [n, 7]
+    post = cs.count_posterior[0].double().cpu().numpy()
+    rl = np.array([x["logZ"] for x in rr])
+    rp = np.array([x["count_posterior"] for x in rr])
+    np.testing.assert_allclose(lz[:, 0], cfg["loglik_empty"], rtol=1e-5)
+    for s in range(1, 7):
+        d = lz[:, s].mean() - rl[:, s].mean()
+        assert abs(d) <= 3 * _se(lz[:, s], rl[:, s]) + 1e-3, (s, lz[:, s].mean(), rl[:, s].mean())
+        assert abs(d) <= 0.01 * abs(rl[:, s].mean()), (s, lz[:, s].mean(), rl[:, s].mean())
+    se = np.sqrt(post.var(0, ddof=1) / len(post) + rp.var(0, ddof=1) / len(rp))
+    assert np.all(np.abs(post.mean(0) - rp.mean(0)) <= 3 * se + 0.02), (post.mean(0), rp.mean(0))

@@ -20,16 +20,16 @@ DEV = "cuda"
 NO_PSF_CACHE = 2048  # include/smcdet_hip.h
 
 
-def _m71_image(H, seed, n_tiles):
+def _m71_image(H, seed, n_tiles, counts_rate=0.004):
     torch.manual_seed(seed)
-    truth = p_m71_prior(H * n_tiles, 0, 40, counts_rate=0.004)
+    truth = p_m71_prior(H * n_tiles, 0, 40, counts_rate=counts_rate)
     _, l, f = truth.sample(num_catalogs=1, device=DEV)
     return p_m71_model(H * n_tiles).sample(l, f)[0, 0, :, :, 0].contiguous()
 
 
-def _run(img, td, prior, model, mh, N, seed, cache, by_count=False):
+def _run(img, td, prior, model, mh, N, seed, cache, by_count=False, flags=0):
     from smcdet_amd.sampler import SMCsampler
-    mh.debug_flags = 0 if cache else NO_PSF_CACHE
+    mh.debug_flags = flags | (0 if cache else NO_PSF_CACHE)
     s = SMCsampler(img, td, prior, model, mh, N, 0.5, "systematic",
                    M71["flux_detection_threshold"], 200, print_every=10 ** 9, seed=seed,
                    device=DEV)
@@ -45,13 +45,18 @@ def _assert_same(a, b):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
 
 
+@pytest.mark.parametrize("table", [True, False], ids=["psf-table", "exp2"])
 @pytest.mark.parametrize("S", [4, 10])
-def test_psf_cache_m71_8x8_run_is_bit_identical(S):
-    """2x2 grid of 8x8 M71 tiles, N = 1024, K = 50, to temperature 1."""
-    img = _m71_image(8, 21 + S, 2)
-    out = [_run(img, 8, p_m71_prior(8, S, S), p_m71_model(8), p_m71_mh(50), 1024, 5, c)
+def test_psf_cache_m71_8x8_run_is_bit_identical(S, table):
+    """2x2 grid of 8x8 M71 tiles at the real M71 source density, N = 1024,
+    K = 50, to temperature 1 (>= 10 SMC iterations, so the cache's accept-path
+    updates are compared many times over), with the PSF values from the radial
+    table (default) and from exp2/log2 (SMCDET_MH_NO_PSF_TABLE)."""
+    img = _m71_image(8, 21 + S, 2, counts_rate=M71["counts_rate"])
+    fl = 0 if table else NO_PSF_TABLE
+    out = [_run(img, 8, p_m71_prior(8, S, S), p_m71_model(8), p_m71_mh(50), 1024, 5, c, flags=fl)
            for c in (True, False)]
-    assert out[0]["iter"] >= 2
+    assert out[0]["iter"] >= 10, int(out[0]["iter"])
     _assert_same(*out)
 
 
@@ -68,17 +73,22 @@ def test_psf_cache_poisson_8x8_run_is_bit_identical():
 
 
 NO_RCP_CACHE = 4096  # include/smcdet_hip.h
+NO_PSF_TABLE = 8192
 
 
-@pytest.mark.parametrize("H,N", [(32, 1024), (16, 512)])
-def test_rcp_cache_m71_run_is_bit_identical(H, N):
+@pytest.mark.parametrize("H,N,base", [(32, 1024, NO_PSF_TABLE), (16, 512, 0),
+                                      (16, 512, NO_PSF_TABLE)])
+def test_rcp_cache_m71_run_is_bit_identical(H, N, base):
     """M71 tiles of 65..1024 pixels keep a per-wave image of 1/(s0^2 + eta*rate)
     in LDS (read by the pixel delta instead of formed; on accept the delta's
     own reciprocal of the new rate is stored): whole C2-geometry runs are
-    bit-identical with and without it (SMCDET_MH_NO_RCP_CACHE)."""
+    bit-identical with and without it (SMCDET_MH_NO_RCP_CACHE).  At 32x32
+    the PSF table takes the LDS the 1/v image would need, so the cache runs
+    there only without the table (base = SMCDET_MH_NO_PSF_TABLE); 16x16 tiles
+    hold both."""
     img = _m71_image(H, 31 + H, 1)
     out = []
-    for flags in (0, NO_RCP_CACHE):
+    for flags in (base, base | NO_RCP_CACHE):
         from smcdet_amd.sampler import SMCsampler
         mh = p_m71_mh(100)
         mh.debug_flags = flags
@@ -92,3 +102,32 @@ def test_rcp_cache_m71_run_is_bit_identical(H, N):
                                "loglik", "mutation_acc_rates")} | {"iter": np.array(s.iter)})
     assert out[0]["iter"] >= 2
     _assert_same(*out)
+
+
+def test_psf_table_sweep_close_to_exp2_sweep():
+    """The radial PSF table (default for M71 sweeps) against the exp2/log2
+    form (SMCDET_MH_NO_PSF_TABLE) on one C2-geometry sweep from the same state
+    with the same Philox draws: the table's PSF values differ by float32
+    rounding (<= 3e-7 relative), so the two sweeps make the same decisions
+    except at near ties -- and they are not bit-identical (the table path
+    ran)."""
+    from smcdet_amd._rng import PhiloxStream
+    H, N, K = 32, 2048, 100
+    img = _m71_image(H, 77, 1, counts_rate=0.003125)[None, None].contiguous()
+    prior, model = p_m71_prior(H, 10, 10, counts_rate=0.003125), p_m71_model(H)
+    torch.manual_seed(8)
+    counts, locs, fluxes = prior.sample(num_tiles_per_side=1, stratify_by_count=True,
+                                        num_catalogs_per_count=N, device=DEV)
+    tau = torch.tensor([[0.02]], device=DEV)
+    res = []
+    for flags in (0, NO_PSF_TABLE):
+        mh = p_m71_mh(K)
+        mh.debug_flags = flags
+        mh.rng = PhiloxStream(17)
+        lo, fo, _ = mh.run(img, counts, locs, fluxes, tau, prior=prior, image_model=model)
+        res.append((lo.cpu().numpy(), fo.cpu().numpy(), mh.last_loglik.cpu().numpy()))
+    same = np.all(res[0][0] == res[1][0], axis=(-1, -2)) & np.all(res[0][1] == res[1][1], axis=-1)
+    assert same.mean() > 0.97, same.mean()
+    close = np.abs(res[0][2] - res[1][2])[same]
+    assert close.max() < 2e-2, close.max()
+    assert not all(np.array_equal(a, b) for a, b in zip(res[0], res[1]))

@@ -181,7 +181,18 @@ def test_statistical_parity_c2_geometry(which):
     assert abs(e0.mean() - e0_ref.mean()) <= 3 * _se(e0, e0_ref), (e0.mean(), e0_ref.mean())
     print(which, "log Z mean", lz.mean(), "ref", lz_ref.mean(), "median", np.median(lz),
           "ref", np.median(lz_ref), "iters", it.mean(), "ref", it_ref.mean())
-    if which in C2_MODERATE:
+    if which in C2_MODERATE and len(rr) < 20:
+        # a smoke check, not a distributional claim: too few
+        # reference runs (8 at K = 100, ~75 min each) to resolve the log Z
+        # law's lower mode (~8% of the oracle's 48 runs), so no 3-SE mean
+        # gate against them; a rank test and the medians within 1% instead.
+        # The distribution-level claim rests on the "_oracle" target (48
+        # runs: mean within 3 SE and 1%, rank test, lower-mode share) and on
+        # the paired replays of tests/test_gpu_paired.py.
+        assert mannwhitneyu(lz, lz_ref).pvalue > 0.001, (np.median(lz), np.median(lz_ref))
+        assert abs(np.median(lz) - np.median(lz_ref)) <= 0.01 * abs(np.median(lz_ref))
+        assert abs(np.median(it) - np.median(it_ref)) <= max(2.0, 0.15 * np.median(it_ref))
+    elif which in C2_MODERATE:
         se = _se(lz, lz_ref)
         diff = lz.mean() - lz_ref.mean()
         assert abs(diff) <= 3 * se, (lz.mean(), lz_ref.mean(), se)

@@ -1,0 +1,92 @@
+"""The oracle's own random streams, exported for paired replays (CPU).
+
+tests/golden/make_oracle_stats.py runs the reference's algorithm on the CPU
+restatement with its own streams: numpy PCG64 for the prior draw and the
+systematic offsets, splitmix64 per particle inside the C sweep.
+oracle.c_oracle.sweep_draws restates the sweep's stream as replay arrays;
+tests/test_gpu_paired.py feeds them to the GPU sampler.  Here: replaying them
+through the C sweep reproduces the seeded sweep exactly, and the
+replay-driven oracle run reproduces make_oracle_stats.run_one.
+"""
+import numpy as np
+
+from oracle import c_oracle as C
+from oracle import smc_oracle as O
+from tests._params import M71, o_m71_model, o_m71_prior
+
+
+def _state(H, N, S, seed):
+    rng = np.random.default_rng(seed)
+    prior = o_m71_prior(H, S, S)
+    uloc = rng.random((1, 1, N, S, 2), dtype=np.float32)
+    uflux = rng.random((1, 1, N, S), dtype=np.float32)
+    return prior, O.prior_sample_stratified(prior, 1, N, uloc, uflux)
+
+
+def test_sweep_draws_replay_equals_seeded_sweep():
+    H, N, S, K = 8, 64, 4, 30
+    prior, (counts, locs, fluxes) = _state(H, N, S, 3)
+    model = o_m71_model(H)
+    img = np.asarray(O.render_rate(locs[:, :, :1], fluxes[:, :, :1], model),
+                     np.float32)[0, 0, :, :, 0].reshape(1, 1, H, H)
+    mh = O.MHParams(K, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    seed = 0x1234_5678_9ABC
+    a = C.mh_sweep(img, counts, locs, fluxes, 0.4, prior, model, mh, seed=seed, threads=2)
+    d = C.sweep_draws(seed, 1, N, K, S)
+    assert d["comp"].shape == (K, 1, N) and d["comp"].max() < S
+    b = C.mh_sweep(img, counts, locs, fluxes, 0.4, prior, model, mh, replay=d, threads=2)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    assert float(a[2].ravel()[0]) == float(b[2].ravel()[0])
+    # the particles moved (the comparison is not vacuous)
+    assert np.abs(a[0] - locs).max() > 0
+
+
+def test_replayed_oracle_run_equals_make_oracle_stats():
+    """The paired test's driver, run with the oracle's sweep, is
+    make_oracle_stats.run_one: same log Z and iteration count."""
+    from tests.golden.make_oracle_stats import run_one
+    H, N, S, K = 8, 96, 3, 8
+    model = o_m71_model(H)
+    loc = np.array([[[[[3.3, 4.6], [6.1, 1.8]]]]], np.float32)
+    flx = np.array([[[[5.0, 2.0]]]], np.float32)
+    img = np.asarray(O.render_rate(loc, flx, model), np.float32)[0, 0, :, :, 0]
+    cfg = dict(tile=H, N=N, S=S, K=K, rho=0.5, counts_rate=M71["counts_rate"],
+               max_smc_iters=100)
+    ref = run_one(img.tolist(), cfg, 11, 2)
+    out = paired_oracle_run(img, cfg, 11)
+    assert out["iters"] == ref["iters"]
+    assert out["logZ"] == ref["logZ"]
+
+
+def paired_oracle_run(img, cfg, seed):
+    """make_oracle_stats.run_one's schedule with every sweep replaying
+    sweep_draws (the form the GPU paired test drives)."""
+    H, N, S, K = cfg["tile"], cfg["N"], cfg["S"], cfg["K"]
+    model = o_m71_model(H)
+    prior = o_m71_prior(H, S, S, counts_rate=cfg["counts_rate"])
+    mh = O.MHParams(K, 0.1, 2.5, M71["flux_lower"], M71["flux_upper"])
+    tiled = np.asarray(img, np.float32).reshape(1, 1, H, H)
+    rng = np.random.default_rng(seed)
+    uloc = rng.random((1, 1, N, S, 2), dtype=np.float32)
+    uflux = rng.random((1, 1, N, S), dtype=np.float32)
+    counts, locs, fluxes = O.prior_sample_stratified(prior, 1, N, uloc, uflux)
+    tau = np.zeros((1, 1), np.float32)
+    logZ = np.zeros((1, 1), np.float64)
+    ll = C.loglik(tiled, locs, fluxes, model, 2)
+    tau_prev = tau
+    tau, _ = O.temper(ll, tau, cfg["rho"] * N)
+    W, ess, logZ = O.update_weights(ll, tau, tau_prev, logZ, N)
+    it = 0
+    while np.any(tau < 1) and it <= cfg["max_smc_iters"]:
+        it += 1
+        idx = O.systematic_resample_index(W, rng.random((1, 1), dtype=np.float32))
+        counts, locs, fluxes = O.gather_particles(idx, counts, locs, fluxes)
+        d = C.sweep_draws((seed * 1000003 + it) & 0xFFFFFFFFFFFF, 1, N, K, S)
+        locs, fluxes, _ = C.mh_sweep(tiled, counts, locs, fluxes, tau, prior, model, mh,
+                                     replay=d, threads=2)
+        ll = C.loglik(tiled, locs, fluxes, model, 2)
+        tau_prev = tau
+        tau, _ = O.temper(ll, tau, cfg["rho"] * N)
+        W, ess, logZ = O.update_weights(ll, tau, tau_prev, logZ, N)
+    return dict(logZ=float(logZ.flat[0]), iters=it)
