@@ -92,10 +92,11 @@ extern "C" {
 /* diagnostic: M71 tiles of 65..1024 pixels without the per-wave 1/v image
  * (each pixel's 1/(s0^2 + eta*rate) formed per use); same results */
 #define SMCDET_MH_NO_RCP_CACHE 4096u
-/* diagnostic: M71 sweeps without the radial PSF table in LDS (the union
- * window's PSF values by exp2/log2 instead of the cubic table; results differ
- * by float32 rounding of the profile, ~3e-7 relative) */
-#define SMCDET_MH_NO_PSF_TABLE 8192u
+/* diagnostic: M71 sweeps with the radial PSF table in LDS (the union
+ * window's PSF values from a cubic table instead of exp2/log2; results differ
+ * by float32 rounding of the profile, ~3e-7 relative).  Measured slower at
+ * 32x32 (its LDS reads) and even at 8x8, so off by default */
+#define SMCDET_MH_PSF_TABLE 8192u
 
 /* Image model (smcdet/images.py:6-26 ImageModel, :105-145 M71ImageModel). */
 typedef struct smcdet_image_model {

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Radial PSF table (M71 sweeps): the parity / equality tests through it, then
-# a same-box A/B of the C2 and C4 bench lines with and without it
-# (SMCDET_MH_NO_PSF_TABLE = 8192: the exp2/log2 form, with the 1/v cache at
-# 32x32), alternating.  Each GPU step has its own limit; a crash or timeout
+# a same-box A/B of the C2 and C4 bench lines without and with it
+# (SMCDET_MH_PSF_TABLE = 8192, opt-in; the default is the exp2/log2 form, with
+# the 1/v cache at 32x32), alternating.  Each GPU step has its own limit; a crash or timeout
 # ends it.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

@@ -400,7 +400,8 @@ __device__ __forceinline__ f2 psf_raw2(const DevModel& m, f2 r2) {
 // (c0, c1, c2, c3); psi = c0 + t(c1 + t(c2 + t c3)).  One ds_read_b128 and
 // four VALU replace 3 exp2 + 1 log2 per evaluation; the fit error is below
 // float32 rounding (max relative error 3.0e-7, mean 9e-8, against 7.5e-7 /
-// 1.6e-7 for the float32 exp2/log2 form).
+// 1.6e-7 for the float32 exp2/log2 form).  Opt-in (SMCDET_MH_PSF_TABLE): the
+// lanes' scattered b128 reads made the 32x32 sweep 50% slower.
 // The index comes from the float32 round-to-nearest trick: y = u + 1.5*2^23
 // holds round(u) in its low mantissa bits (u < 2^22), y - 1.5*2^23 is that
 // integer exactly, so t is exact too.  CLAMP bounds the index for positions

@@ -1411,7 +1411,7 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
   a.no_psf_cache = (flags & SMCDET_MH_NO_PSF_CACHE) != 0;
   a.no_rcp_cache = (flags & SMCDET_MH_NO_RCP_CACHE) != 0;
   if (a.m.model == SMCDET_MODEL_M71 && !full && !global_tile && !a.scalar_slots &&
-      !(flags & SMCDET_MH_NO_PSF_TABLE)) {
+      (flags & SMCDET_MH_PSF_TABLE)) {
     rc = psf_table_device(*model, a.m, st, &a.psf_tab, &a.tab_inv_h);
     if (rc) return rc;
   }

@@ -9,11 +9,26 @@ offsets, splitmix64 per particle and SMC iteration in the sweep.  Here the
 GPU sampler replays exactly those draws (oracle.c_oracle.sweep_draws, pinned
 against the C sweep by tests/test_oracle_paired.py) through the reference's
 loop (smcdet/sampler.py:221-256: resample -> mutate -> temper ->
-update_weights), so each GPU run is the oracle run's twin.  Trajectories can
-still part where a float32 decision differs from the float64 one (a near
-tie), so the comparison is per run: the same log Z mode (the lower mode sits
-~65 nats below the main one, make_oracle_stats' 4 of 48) in >= 46 of 48 runs,
-and |delta log Z| far below the mode gap.
+update_weights), so each GPU run is the oracle run's twin.
+
+Twins part where a float32 decision differs from the float64 one (a near
+tie among ~7M decisions per run): the temperature ladders agree for the
+first iterations and leave each other at iteration 3-12
+(scripts/paired_bisect.py, profiles/r04/paired_bisect.json) -- in every
+variant, the reference's own float32 full re-render and a GPU run tempered
+by the oracle's float64 tile pass included.  From there on a twin is a new
+draw of the run's random outcome, so on "fragile" seeds (oracle log Z
+between the modes) the mode is not a function of the draws.  The test
+therefore checks:
+  * the pairing: ladders equal (|delta tau| <= 1e-5) for the first two
+    iterations in >= 90% of runs;
+  * agreement where runs are robust: the same mode (cut: median - 40 nats; the
+    lower mode sits ~65-80 nats below) in >= 40 of 48 runs, and median
+    |delta log Z| <= 5 nats over the runs in the same mode;
+  * no systematic excess: McNemar's exact test on the runs in different
+    modes (GPU lower only vs oracle lower only), two-sided p > 0.01.
+The reference-arithmetic twin (SingleComponentMH(full_recompute=True)) is
+recorded next to it as a control (SMCDET_PAIRED_OUT summary).
 """
 import json
 import os
@@ -36,13 +51,13 @@ def _target():
         return json.load(f)
 
 
-def paired_gpu_run(img, cfg, seed):
+def paired_gpu_run(img, cfg, seed, full_recompute=False):
     """make_oracle_stats.run_one's schedule and streams on the GPU sampler."""
     from oracle import c_oracle as C
     from smcdet_amd.sampler import SMCsampler
     H, N, S, K = cfg["tile"], cfg["N"], cfg["S"], cfg["K"]
     prior = p_m71_prior(H, S, S, counts_rate=cfg["counts_rate"])
-    model, mh = p_m71_model(H), p_m71_mh(K)
+    model, mh = p_m71_model(H), p_m71_mh(K, full_recompute=full_recompute)
     image = torch.tensor(img, dtype=torch.float32, device=DEV)
     s = SMCsampler(image, H, prior, model, mh, N, cfg["rho"], "systematic",
                    M71["flux_detection_threshold"], cfg["max_smc_iters"], print_every=10 ** 9,
@@ -58,6 +73,7 @@ def paired_gpu_run(img, cfg, seed):
     s.temper()
     s.update_weights()
     s.iter = 0
+    taus = [float(s.temperature.flatten()[0])]
     while bool((s.temperature < 1).any()) and s.iter <= s.max_smc_iters:
         s.iter += 1
         u = torch.from_numpy(rng.random((1, 1), dtype=np.float32)).to(DEV)
@@ -71,8 +87,9 @@ def paired_gpu_run(img, cfg, seed):
         s._fresh_loglik = mh.last_loglik
         s.temper()
         s.update_weights()
+        taus.append(float(s.temperature.flatten()[0]))
     return dict(seed=seed, logZ=float(s.log_normalizing_constant.flatten()[0]), iters=s.iter,
-                final_ess=float(s.ess.flatten()[0]))
+                final_ess=float(s.ess.flatten()[0]), tau=taus)
 
 
 @pytest.mark.parametrize("chunk", range(CHUNKS))
@@ -81,10 +98,38 @@ def test_paired_runs_chunk(chunk):
     runs = ref["runs"]
     for r in runs[chunk::CHUNKS]:
         out = paired_gpu_run(ref["image"], ref["config"], r["seed"])
+        full = paired_gpu_run(ref["image"], ref["config"], r["seed"], full_recompute=True)
+        out["full_logZ"], out["full_iters"] = full["logZ"], full["iters"]
         out["oracle_logZ"], out["oracle_iters"] = r["logZ"], r["iters"]
+        ot, gt = r["tau_trace"], out["tau"]
+        n = min(len(ot), len(gt))
+        off = [i for i in range(n) if abs(ot[i] - gt[i]) > 1e-5]
+        out["first_tau_divergence"] = off[0] if off else n
         _results[r["seed"]] = out
-        print(f"seed {r['seed']}: GPU log Z {out['logZ']:.2f} ({out['iters']} it), oracle "
-              f"{r['logZ']:.2f} ({r['iters']} it)", flush=True)
+        print(f"seed {r['seed']}: GPU log Z {out['logZ']:.2f} ({out['iters']} it), full re-render "
+              f"{full['logZ']:.2f}, oracle {r['logZ']:.2f} ({r['iters']} it); ladders part at "
+              f"iteration {out['first_tau_divergence']}", flush=True)
+
+
+def _mcnemar_p(b, c):
+    """Exact two-sided McNemar p-value for b vs c discordant pairs."""
+    from math import comb
+    n, k = b + c, min(b, c)
+    if n == 0:
+        return 1.0
+    return min(1.0, 2.0 * sum(comb(n, i) for i in range(k + 1)) / 2.0 ** n)
+
+
+def _compare(lz, lz_o, cut):
+    low, low_o = lz < cut, lz_o < cut
+    same = low == low_o
+    d = lz - lz_o
+    b, c = int((low & ~low_o).sum()), int((~low & low_o).sum())
+    return dict(same_mode=int(same.sum()), lower_only_here=b, lower_only_oracle=c,
+                mcnemar_p=_mcnemar_p(b, c), lower_mode=int(low.sum()),
+                lower_mode_oracle=int(low_o.sum()),
+                abs_dlogz_median_same_mode=float(np.median(np.abs(d[same]))),
+                abs_dlogz_p90=float(np.percentile(np.abs(d), 90)), mean_dlogz=float(d.mean()))
 
 
 def test_paired_runs_same_mode():
@@ -95,19 +140,23 @@ def test_paired_runs_same_mode():
     lz_o = np.array([r["logZ"] for r in runs])
     cut = float(np.median(lz_o) - 40.0)
     res = [_results[r["seed"]] for r in runs]
-    lz_g = np.array([x["logZ"] for x in res])
-    same = (lz_g < cut) == (lz_o < cut)
-    dl = lz_g - lz_o
-    summary = dict(cut=cut, n=len(res), same_mode=int(same.sum()),
-                   lower_mode_oracle=int((lz_o < cut).sum()), lower_mode_gpu=int((lz_g < cut).sum()),
-                   abs_dlogz_median=float(np.median(np.abs(dl))),
-                   abs_dlogz_p90=float(np.percentile(np.abs(dl), 90)),
-                   mean_dlogz=float(dl.mean()), runs=res)
+    gpu = _compare(np.array([x["logZ"] for x in res]), lz_o, cut)
+    full = _compare(np.array([x["full_logZ"] for x in res]), lz_o, cut)
+    twins = _compare(np.array([x["logZ"] for x in res]), np.array([x["full_logZ"] for x in res]),
+                     cut)
+    first = np.array([x["first_tau_divergence"] for x in res])
+    summary = dict(cut=cut, n=len(res), gpu_vs_oracle=gpu, full_recompute_vs_oracle=full,
+                   gpu_vs_full_recompute=twins,
+                   ladder_first_divergence={"min": int(first.min()),
+                                            "median": float(np.median(first)),
+                                            "share_ge_2": float((first >= 2).mean())},
+                   runs=res)
     path = os.environ.get("SMCDET_PAIRED_OUT")
     if path:
         with open(path, "w") as f:
             json.dump(summary, f, indent=1)
     print({k: v for k, v in summary.items() if k != "runs"})
-    assert same.sum() >= len(res) - 2, summary
-    # the runs in the same mode: log Z differences far below the ~65-nat gap
-    assert np.median(np.abs(dl[same])) < 10.0, summary
+    assert (first >= 2).mean() >= 0.9, summary["ladder_first_divergence"]
+    assert gpu["same_mode"] >= len(res) - 8, gpu
+    assert gpu["abs_dlogz_median_same_mode"] <= 5.0, gpu
+    assert gpu["mcnemar_p"] > 0.01, gpu

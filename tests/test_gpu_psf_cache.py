@@ -18,6 +18,7 @@ from tests._params import (M71, p_basic_mh, p_basic_model, p_basic_prior, p_m71_
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 NO_PSF_CACHE = 2048  # include/smcdet_hip.h
+PSF_TABLE = 8192
 
 
 def _m71_image(H, seed, n_tiles, counts_rate=0.004):
@@ -50,10 +51,10 @@ def _assert_same(a, b):
 def test_psf_cache_m71_8x8_run_is_bit_identical(S, table):
     """2x2 grid of 8x8 M71 tiles at the real M71 source density, N = 1024,
     K = 50, to temperature 1 (>= 10 SMC iterations, so the cache's accept-path
-    updates are compared many times over), with the PSF values from the radial
-    table (default) and from exp2/log2 (SMCDET_MH_NO_PSF_TABLE)."""
+    updates are compared many times over), with the PSF values from exp2/log2
+    (default) and from the opt-in radial table (SMCDET_MH_PSF_TABLE)."""
     img = _m71_image(8, 21 + S, 2, counts_rate=M71["counts_rate"])
-    fl = 0 if table else NO_PSF_TABLE
+    fl = PSF_TABLE if table else 0
     out = [_run(img, 8, p_m71_prior(8, S, S), p_m71_model(8), p_m71_mh(50), 1024, 5, c, flags=fl)
            for c in (True, False)]
     assert out[0]["iter"] >= 10, int(out[0]["iter"])
@@ -73,19 +74,16 @@ def test_psf_cache_poisson_8x8_run_is_bit_identical():
 
 
 NO_RCP_CACHE = 4096  # include/smcdet_hip.h
-NO_PSF_TABLE = 8192
 
 
-@pytest.mark.parametrize("H,N,base", [(32, 1024, NO_PSF_TABLE), (16, 512, 0),
-                                      (16, 512, NO_PSF_TABLE)])
+@pytest.mark.parametrize("H,N,base", [(32, 1024, 0), (16, 512, 0), (16, 512, PSF_TABLE)])
 def test_rcp_cache_m71_run_is_bit_identical(H, N, base):
     """M71 tiles of 65..1024 pixels keep a per-wave image of 1/(s0^2 + eta*rate)
     in LDS (read by the pixel delta instead of formed; on accept the delta's
     own reciprocal of the new rate is stored): whole C2-geometry runs are
-    bit-identical with and without it (SMCDET_MH_NO_RCP_CACHE).  At 32x32
-    the PSF table takes the LDS the 1/v image would need, so the cache runs
-    there only without the table (base = SMCDET_MH_NO_PSF_TABLE); 16x16 tiles
-    hold both."""
+    bit-identical with and without it (SMCDET_MH_NO_RCP_CACHE); 16x16 tiles
+    also with the opt-in PSF table (SMCDET_MH_PSF_TABLE), which at 32x32 takes
+    the LDS the 1/v image needs."""
     img = _m71_image(H, 31 + H, 1)
     out = []
     for flags in (base, base | NO_RCP_CACHE):
@@ -105,8 +103,8 @@ def test_rcp_cache_m71_run_is_bit_identical(H, N, base):
 
 
 def test_psf_table_sweep_close_to_exp2_sweep():
-    """The radial PSF table (default for M71 sweeps) against the exp2/log2
-    form (SMCDET_MH_NO_PSF_TABLE) on one C2-geometry sweep from the same state
+    """The opt-in radial PSF table (SMCDET_MH_PSF_TABLE) against the default
+    exp2/log2 form on one C2-geometry sweep from the same state
     with the same Philox draws: the table's PSF values differ by float32
     rounding (<= 3e-7 relative), so the two sweeps make the same decisions
     except at near ties -- and they are not bit-identical (the table path
@@ -120,7 +118,7 @@ def test_psf_table_sweep_close_to_exp2_sweep():
                                         num_catalogs_per_count=N, device=DEV)
     tau = torch.tensor([[0.02]], device=DEV)
     res = []
-    for flags in (0, NO_PSF_TABLE):
+    for flags in (PSF_TABLE, 0):
         mh = p_m71_mh(K)
         mh.debug_flags = flags
         mh.rng = PhiloxStream(17)
