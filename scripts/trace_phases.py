@@ -21,8 +21,7 @@ from smcdet_amd import _hip  # noqa: E402
 from smcdet_amd.sampler import SMCsampler  # noqa: E402
 
 MH_PHASES = ["stage image", "state + tn caches", "initial render", "MH loop", "write back"]
-TILE_PHASES = ["load ll + max", "f(top)", "brentq", "weights", "cumsum", "slot zero",
-               "slot scatter", "prefix max", "store idx"]
+TILE_PHASES = ["load ll + max", "f(top)", "brentq", "weights", "cumsum", "index search + store"]
 
 
 def read(name, cols):
@@ -53,7 +52,7 @@ def main():
         s._step(idx)  # (two launches: the sweep, then the tile kernel)
         torch.cuda.synchronize()
         mh_d = read("smcdet_trace_read_mh", 6)
-        tile_d = read("smcdet_trace_read_tile", 10)[:1]
+        tile_d = read("smcdet_trace_read_tile", len(TILE_PHASES) + 1)[:1]
         out[f"step{i}"] = {
             "tau": float(s.temperature.min()),
             "mh_cycles_mean": dict(zip(MH_PHASES, mh_d.mean(0).round(0).tolist())),

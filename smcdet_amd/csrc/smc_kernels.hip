@@ -4,26 +4,36 @@
 // tile), gather, pruning (sampler.py:198-219), the CS-SMC count posterior and
 // the aggregation temper / reweight kernels.
 #include <math.h>
+#include <stdlib.h>
+
+#include <type_traits>
 
 #include "tile.h"
 
 namespace smcdet {
 
 
-// One workgroup of kTileNT threads per tile, on tile.h's 512-thread virtual
-// layout (so any kTileNT gives the same results; the MH sweep's fused tail
-// runs the same work on its 256 threads).
-#ifndef SMCDET_TILE_NT
-#define SMCDET_TILE_NT 512
-#endif
-constexpr int kTileNT = SMCDET_TILE_NT;
-template <int PER>
-__global__ __launch_bounds__(kTileNT) void tile_kernel(TileArgs a) {
+// One workgroup of NT threads per tile, on tile.h's 512-thread virtual
+// layout, so either NT gives the same results bit for bit (the MH sweep's
+// fused tail runs the same work on its 256 threads).  512 by default;
+// SMCDET_TILE_THREADS=256 in the environment selects the 256-thread
+// instantiation (A/B: fewer waves at each Brent barrier, two virtual threads
+// per thread).
+template <int NT, int PER>
+__global__ __launch_bounds__(NT) void tile_kernel(TileArgs a) {
   if (a.go && *a.go == 0) return;  // speculatively enqueued iteration that must not run
   extern __shared__ float buf[];  // N floats: weights / cumsum, then N+1 resample slots
   __shared__ TileRed red;
   const int t = blockIdx.x;
-  tile_work<kTileNT, PER>(a, t, buf, red, threadIdx.x < kWave ? t : -1);
+  tile_work<NT, PER>(a, t, buf, red, threadIdx.x < kWave ? t : -1);
+}
+
+static int tile_threads() {
+  static const int nt = [] {
+    const char* e = getenv("SMCDET_TILE_THREADS");
+    return (e && atoi(e) == 256) ? 256 : 512;
+  }();
+  return nt;
 }
 
 // gather: thread per (t, n, s)
@@ -327,16 +337,22 @@ static int launch_tile(const TileArgs& a, hipStream_t st) {
   // weights / bins, then (systematic resampling) N+1 slots
   const size_t lds = (size_t)(2 * a.N + 1) * sizeof(float);
   const int per = (a.N + kTB - 1) / kTB;
-  const void* fn = per <= 1 ? (const void*)tile_kernel<1>
-                 : per <= 2 ? (const void*)tile_kernel<2>
-                 : per <= 4 ? (const void*)tile_kernel<4>
-                 : per <= 8 ? (const void*)tile_kernel<8>
-                 : per <= 16 ? (const void*)tile_kernel<16>
-                             : (const void*)tile_kernel<32>;
+  const int nt = tile_threads();
+  auto pick = [per](auto NT) -> const void* {
+    constexpr int n = decltype(NT)::value;
+    return per <= 1 ? (const void*)tile_kernel<n, 1>
+         : per <= 2 ? (const void*)tile_kernel<n, 2>
+         : per <= 4 ? (const void*)tile_kernel<n, 4>
+         : per <= 8 ? (const void*)tile_kernel<n, 8>
+         : per <= 16 ? (const void*)tile_kernel<n, 16>
+                     : (const void*)tile_kernel<n, 32>;
+  };
+  const void* fn = nt == 256 ? pick(std::integral_constant<int, 256>{})
+                             : pick(std::integral_constant<int, 512>{});
   int rc = ensure_lds(fn, lds + sizeof(TileRed));
   if (rc) return rc;
   void* args[] = {const_cast<TileArgs*>(&a)};
-  hipError_t e = hipLaunchKernel(fn, dim3(a.T), dim3(kTileNT), args, lds, st);
+  hipError_t e = hipLaunchKernel(fn, dim3(a.T), dim3(nt), args, lds, st);
   if (e != hipSuccess) return set_error(SMCDET_EHIP, "tile kernel launch: %s", hipGetErrorString(e));
   return check_launch("smcdet tile kernel");
 }

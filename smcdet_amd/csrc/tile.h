@@ -598,7 +598,7 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
           if (n < N) idxg[n] = (int64_t)min(lo[g], N - 1);
         }
       }
-      SMC_TRACE(trow, 9);
+      SMC_TRACE(trow, 6);
     } else {
       // multinomial (sampler.py:127-140): target = u * total, first bin > target
       for (int n = threadIdx.x; n < N; n += NT) {
