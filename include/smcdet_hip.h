@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 15
+#define SMCDET_ABI_VERSION 16
 
 /* status codes */
 #define SMCDET_OK 0
@@ -389,6 +389,16 @@ typedef struct smcdet_smc_tail {
   int32_t* live_host;
   int32_t iter;
   int32_t reserved;
+  /* (ABI 16) systematic resampling handed to the next sweep as bins instead
+   * of indices: bins_out [T*N + T] (nullable) receives the tile's running sum
+   * of the new weights (float32 roundings of the float64 cumsum) followed by
+   * the T offsets U -- the tile pass then skips the index search; anc_bins
+   * (nullable, input) is such a buffer from the previous step, and each wave
+   * of this sweep finds its own ancestor in it (idx[n] = #{i : bins[i] <
+   * (n + U)/N}, clamped to N - 1: the same indices, bit for bit) in place of
+   * `ancestors`.  smcdet_bins_index converts a buffer to the indices. */
+  const float* anc_bins;
+  float* bins_out;
 } smcdet_smc_tail_t;
 
 /* One SMC iteration of SMCsampler.run (smcdet/sampler.py:221-237: resample
@@ -419,6 +429,11 @@ int smcdet_mh_sweep_step_fused(const smcdet_image_model_t* model, int32_t N,
                                int32_t S, uint32_t flags);
 
 /* Gather of the resampled state (smcdet/sampler.py:150-169). */
+/* The systematic resampling indices [T,N] of a bins buffer (the tail's
+ * bins_out layout: [T*N] running sums, then [T] offsets U): idx[t,n] =
+ * #{i : bins[t,i] < (n + U_t)/N} clamped to N - 1 (sampler.py:141-148). */
+int smcdet_bins_index(const float* bins, int32_t T, int32_t N, int64_t* idx, void* stream);
+
 int smcdet_gather(const int64_t* idx, int32_t T, int32_t N, int32_t S,
                   const float* counts_in, const float* locs_in,
                   const float* fluxes_in, float* counts_out, float* locs_out,

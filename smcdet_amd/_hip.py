@@ -23,7 +23,7 @@ SMCDET_RESAMPLE_SYSTEMATIC = 1
 SMCDET_MH_FULL_RECOMPUTE = 1
 SMCDET_MH_COMPONENT_BY_COUNT = 2
 SMCDET_MH_SKIP_DONE = 4
-ABI_VERSION = 15
+ABI_VERSION = 16
 SMCDET_SMC_FREEZE_DONE = 1
 SMCDET_SMC_TWO_LAUNCH = 2
 
@@ -106,7 +106,8 @@ class SmcTailC(ctypes.Structure):
                 ("ess", c_p), ("log_norm_const", c_p), ("ess_threshold", c_d),
                 ("resample_method", c_i), ("flags", c_u32), ("seed", c_u64), ("offset", c_u64),
                 ("idx", c_p), ("resample_u", c_p), ("finished_iter", c_p), ("live", c_p),
-                ("live_host", c_p), ("iter", c_i), ("reserved", c_i)]
+                ("live_host", c_p), ("iter", c_i), ("reserved", c_i),
+                ("anc_bins", c_p), ("bins_out", c_p)]
 
 
 _SIGS = {
@@ -143,6 +144,7 @@ _SIGS = {
     "smcdet_temper_reweight": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_d, c_i, c_u64,
                                 c_u64, c_p, c_u32, c_p, c_i, c_p, c_p, c_p, c_p], c_i),
     "smcdet_gather": ([c_p, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
+    "smcdet_bins_index": ([c_p, c_i, c_i, c_p, c_p], c_i),
     "smcdet_count_posterior": ([c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_u64, c_u64, c_p,
                                 c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
     "smcdet_prune": ([c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p, c_p, c_p, c_p], c_i),
@@ -182,6 +184,7 @@ _OUTS = {
     "smcdet_resample_index": ((7,), ()),
     "smcdet_temper_reweight": ((1, 2, 3, 4, 5, 6, 13, 15, 17), ()),
     "smcdet_gather": ((7, 8, 9), ()),
+    "smcdet_bins_index": ((3,), ()),
     "smcdet_count_posterior": ((16, 17, 18, 19, 20), ()),
     "smcdet_prune": ((7, 8, 9), ()),
     "smcdet_aggregate_sweep": ((13, 14, 15, 19, 20, 21, 22, 24), ((10, 13), (11, 14), (12, 15))),
@@ -205,9 +208,12 @@ def check_aliases(name, args):
     spec = _OUTS.get(name)
     if spec is None:
         return
+    addrs = [_addr(a) for a in args[:-1]]
+    nz = [a for a in addrs if a]
+    if len(set(nz)) == len(nz):
+        return  # no pointer repeats (the common case: one set() on the host path)
     outs, inplace = spec
     ok = {frozenset(pq) for pq in inplace}
-    addrs = [_addr(a) for a in args[:-1]]
     for o in outs:
         if o >= len(addrs) or not addrs[o]:
             continue
@@ -377,6 +383,41 @@ def dev_f32(t, name):
 
 def ref(x):
     return ctypes.byref(x)
+
+
+class AncestorBins:
+    """The next systematic resampling as the MH sweep reads it
+    (smcdet_smc_tail_t.anc_bins / bins_out, ABI 16): per tile the running
+    sum of the weights (float32) and the offset U, [T*N + T] float32 -- each
+    wave of the next sweep searches its own ancestor, so the tile pass skips
+    the index search.  to_index() gives the [numH, numW, N] int64 indices (the
+    same ones, bit for bit)."""
+
+    def __init__(self, buf, shape):
+        self.buf = buf
+        self.shape = tuple(shape)  # (numH, numW, N)
+
+    @staticmethod
+    def empty(shape, device):
+        nH, nW, N = shape
+        return AncestorBins(torch.empty(nH * nW * N + nH * nW, device=device,
+                                        dtype=torch.float32), shape)
+
+    def to_index(self):
+        nH, nW, N = self.shape
+        idx = torch.empty(self.shape, device=self.buf.device, dtype=torch.int64)
+        check(lib().smcdet_bins_index(ptr(self.buf), nH * nW, N, ptr(idx), stream_of(idx)),
+              "smcdet_bins_index")
+        return idx
+
+    @property
+    def device(self):
+        return self.buf.device
+
+
+def as_index(x):
+    """Resampling indices of x (an int64 tensor, or AncestorBins), or None."""
+    return x.to_index() if isinstance(x, AncestorBins) else x
 
 
 class HostInts:

@@ -73,6 +73,7 @@ struct MhArgs {
   const float* img;                  // [T,H,W]
   const float* temperature;          // [T]
   const int64_t* ancestors;          // [T,N] or null
+  const float* anc_bins;             // [T*N + T] systematic bins + offsets (bins_ancestor) or null
   const float* counts_in;
   const float* locs_in;
   const float* fluxes_in;
@@ -385,7 +386,10 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
 
   const int N = a.N, S = a.S;
   const size_t pid = (size_t)t * N + n;
-  const size_t src = a.ancestors ? (size_t)t * N + (size_t)a.ancestors[pid] : pid;
+  size_t src = a.ancestors ? (size_t)t * N + (size_t)a.ancestors[pid] : pid;
+  if (a.anc_bins)  // the wave finds its ancestor in the previous tile pass's bins
+    src = (size_t)t * N +
+          (size_t)bins_ancestor(a.anc_bins + (size_t)t * N, N, a.anc_bins[(size_t)a.T * N + t], n);
   if constexpr (GL) lam = a.rate_out + pid * (size_t)HWp;
   const float count = a.counts_in[src];
   if (a.counts_out && lane == 0) a.counts_out[pid] = count;
@@ -1360,46 +1364,60 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
       ((model->model == SMCDET_MODEL_POISSON ? 2 : 1) * HWp + (size_t)kMhWaves * HWp) *
       sizeof(float);
   const dim3 grid((N + kMhWaves - 1) / kMhWaves, T);
-  bool split_tail = false;  // the tile pass as its own launch(es) after the sweep
+  bool split_tail = false;  // the tile pass as its own launch after the sweep
+  TileArgs ta{};
   if (tail) {
     if (!loglik_out) return set_error(SMCDET_EINVAL, "the fused step needs loglik_out");
     if (!tail->temperature_prev || !tail->log_weights_unnorm || !tail->weights || !tail->ess ||
         !tail->log_norm_const)
       return set_error(SMCDET_EINVAL, "null tail buffer");
-    if (tail->idx && tail->resample_method != SMCDET_RESAMPLE_MULTINOMIAL &&
+    if ((tail->idx || tail->bins_out) && tail->resample_method != SMCDET_RESAMPLE_MULTINOMIAL &&
         tail->resample_method != SMCDET_RESAMPLE_SYSTEMATIC)
       return set_error(SMCDET_EINVAL, "unknown resample method %d", tail->resample_method);
     if (tail->resample_u && tail->resample_method != SMCDET_RESAMPLE_SYSTEMATIC)
       return set_error(SMCDET_EINVAL, "resample_u replays systematic resampling only");
+    if (tail->bins_out && tail->resample_method != SMCDET_RESAMPLE_SYSTEMATIC)
+      return set_error(SMCDET_EINVAL, "bins_out hands over systematic resampling only");
+    if (tail->bins_out && tail->idx)
+      return set_error(SMCDET_EINVAL, "tail: idx or bins_out, not both");
+    if (tail->anc_bins && ancestors)
+      return set_error(SMCDET_EINVAL, "ancestors or tail->anc_bins, not both");
+    if (tail->anc_bins && (locs_in == locs_out || fluxes_in == fluxes_out ||
+                           (counts_out && counts_in == counts_out) ||
+                           (rate_in && rate_in == rate_out)))
+      return set_error(SMCDET_EINVAL, "ancestor gather needs distinct in/out buffers");
+    a.anc_bins = tail->anc_bins;
+    ta.flags = kDoTemper | kDoWeights | ((tail->idx || tail->bins_out) ? kDoResample : 0u);
+    ta.T = T;
+    ta.N = N;
+    ta.ess_threshold = tail->ess_threshold;
+    ta.loglik = loglik_out;
+    ta.temperature = const_cast<float*>(temperature);
+    ta.temperature_prev = tail->temperature_prev;
+    ta.log_w = tail->log_weights_unnorm;
+    ta.weights = tail->weights;
+    ta.ess = tail->ess;
+    ta.logZ = tail->log_norm_const;
+    ta.method = tail->resample_method;
+    ta.k0 = (uint32_t)tail->seed;
+    ta.k1 = (uint32_t)(tail->seed >> 32);
+    ta.offset = tail->offset;
+    ta.u = tail->resample_u;
+    ta.idx = tail->idx;
+    ta.bins_out = tail->bins_out;
+    ta.smc_flags = tail->flags & ~SMCDET_SMC_TWO_LAUNCH;
+    ta.fin_iter = tail->finished_iter;
+    ta.iter = tail->iter;
+    ta.live = tail->live;
+    ta.live_host = tail->live ? tail->live_host : nullptr;
     size_t lds_f = 0;
     if (!(tail->flags & SMCDET_SMC_TWO_LAUNCH) && tail_fusable(*model, N, S, flags, &lds_f)) {
-      TileArgs& ta = a.tail;
-      ta.flags = kDoTemper | kDoWeights | (tail->idx ? kDoResample : 0u);
-      ta.T = T;
-      ta.N = N;
-      ta.ess_threshold = tail->ess_threshold;
-      ta.loglik = loglik_out;
-      ta.temperature = const_cast<float*>(temperature);
-      ta.temperature_prev = tail->temperature_prev;
-      ta.log_w = tail->log_weights_unnorm;
-      ta.weights = tail->weights;
-      ta.ess = tail->ess;
-      ta.logZ = tail->log_norm_const;
-      ta.method = tail->resample_method;
-      ta.k0 = (uint32_t)tail->seed;
-      ta.k1 = (uint32_t)(tail->seed >> 32);
-      ta.offset = tail->offset;
-      ta.u = tail->resample_u;
-      ta.idx = tail->idx;
-      ta.smc_flags = tail->flags & ~SMCDET_SMC_TWO_LAUNCH;
-      ta.fin_iter = tail->finished_iter;
-      ta.iter = tail->iter;
-      ta.live = tail->live;
-      ta.go = nullptr;  // the sweep already returned when *go == 0
-      ta.live_host = tail->live ? tail->live_host : nullptr;
+      a.tail = ta;
+      a.tail.go = nullptr;  // the sweep already returned when *go == 0
       a.has_tail = 1;
       lds = lds_f;
     } else {
+      ta.go = go;
       split_tail = true;
     }
   }
@@ -1421,24 +1439,9 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
   if (rc) return rc;
   rc = check_launch("smcdet_mh_sweep");
   if (rc || !split_tail) return rc;
-  float* temp = const_cast<float*>(temperature);
-  const uint32_t smc_flags = tail->flags & ~SMCDET_SMC_TWO_LAUNCH;
-  if (tail->resample_u && tail->idx) {
-    rc = smcdet_temper_reweight(loglik_out, temp, tail->temperature_prev,
-                                tail->log_weights_unnorm, tail->weights, tail->ess,
-                                tail->log_norm_const, T, N, tail->ess_threshold,
-                                tail->resample_method, tail->seed, tail->offset, nullptr,
-                                smc_flags, tail->finished_iter, tail->iter, tail->live, go,
-                                tail->live_host, stream);
-    if (rc) return rc;
-    return smcdet_resample_index(tail->weights, T, N, tail->resample_method, tail->seed,
-                                 tail->offset, tail->resample_u, tail->idx, stream);
-  }
-  return smcdet_temper_reweight(loglik_out, temp, tail->temperature_prev, tail->log_weights_unnorm,
-                                tail->weights, tail->ess, tail->log_norm_const, T, N,
-                                tail->ess_threshold, tail->resample_method, tail->seed,
-                                tail->offset, tail->idx, smc_flags, tail->finished_iter,
-                                tail->iter, tail->live, go, tail->live_host, stream);
+  // the tile pass on the sweep's log-likelihoods (tile.h tile_work: the same
+  // work as smcdet_temper_reweight, replayed offsets and bins included)
+  return launch_tile(ta, st);
 }
 
 extern "C" int smcdet_mh_sweep(const smcdet_image_model_t* model, const smcdet_prior_t* prior,

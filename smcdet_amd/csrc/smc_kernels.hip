@@ -331,7 +331,7 @@ __global__ __launch_bounds__(kTB) void agg_reweight_kernel(AggTileArgs a) {
   }
 }
 
-static int launch_tile(const TileArgs& a, hipStream_t st) {
+int launch_tile(const TileArgs& a, hipStream_t st) {
   if (a.N > kMaxN)
     return set_error(SMCDET_EUNSUPPORTED, "N=%d particles per tile > %d", a.N, kMaxN);
   // weights / bins, then (systematic resampling) N+1 slots
@@ -355,6 +355,16 @@ static int launch_tile(const TileArgs& a, hipStream_t st) {
   hipError_t e = hipLaunchKernel(fn, dim3(a.T), dim3(nt), args, lds, st);
   if (e != hipSuccess) return set_error(SMCDET_EHIP, "tile kernel launch: %s", hipGetErrorString(e));
   return check_launch("smcdet tile kernel");
+}
+
+// bins -> indices: one wave per particle (bins_ancestor), 4 per workgroup
+__global__ __launch_bounds__(256) void bins_index_kernel(const float* __restrict__ bins, int T,
+                                                         int N, int64_t* __restrict__ idx) {
+  const int t = blockIdx.y;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  const int a = bins_ancestor(bins + (size_t)t * N, N, bins[(size_t)T * N + t], n);
+  if ((threadIdx.x & 63) == 0) idx[(size_t)t * N + n] = a;
 }
 
 }  // namespace smcdet
@@ -460,6 +470,14 @@ int smcdet_temper_reweight(const float* loglik, float* temperature, float* tempe
   a.go = go;
   a.live_host = live ? live_host : nullptr;
   return launch_tile(a, (hipStream_t)stream);
+}
+
+int smcdet_bins_index(const float* bins, int32_t T, int32_t N, int64_t* idx, void* stream) {
+  if (!bins || !idx) return set_error(SMCDET_EINVAL, "null buffer");
+  if (T <= 0 || N <= 0 || T > 65535) return set_error(SMCDET_EUNSUPPORTED, "T=%d N=%d", T, N);
+  hipLaunchKernelGGL(bins_index_kernel, dim3((unsigned)((N + 3) / 4), (unsigned)T), dim3(256), 0,
+                     (hipStream_t)stream, bins, T, N, idx);
+  return check_launch("smcdet_bins_index");
 }
 
 int smcdet_gather(const int64_t* idx, int32_t T, int32_t N, int32_t S, const float* counts_in,

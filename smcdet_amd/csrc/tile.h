@@ -59,7 +59,41 @@ struct TileArgs {
   int32_t* live;             // [3] zeroed workspace: counter, ticket, tiles still below 1 (or null)
   const int32_t* go;         // predicate: skip the launch when *go == 0 (or null)
   int32_t* live_host;        // host-mapped copy of live[2] (pinned host memory) or null
+  float* bins_out;           // [T*N + T] systematic bins + offsets instead of idx (or null)
 };
+
+// one tile pass launch (smc_kernels.hip)
+int launch_tile(const TileArgs& a, hipStream_t st);
+
+// The systematic ancestor of particle n, idx[n] = #{i : bins[i] < u_n}
+// clamped to N - 1, u_n = (n + U)/N in float32 (sampler.py:141-148), found by
+// the 64 lanes of a wave in the monotone bins (global memory, L2-resident): a
+// 64-ary search, log64(N) dependent loads (two at N = 4096).  The test is
+// the tile pass's (bins[i] < u_n, for N a power of two as b*N < fl(n + U),
+// exact), so the index is the one the tile pass's search would write.  Call
+// from converged code; the result is wave-uniform.
+__device__ __forceinline__ int bins_ancestor(const float* __restrict__ bins, int N, float U,
+                                             int n) {
+  const int lane = threadIdx.x & 63;
+  const float Nf = (float)N;
+  const bool pow2 = (N & (N - 1)) == 0;
+  const float nu = (float)n + U;
+  const float key = pow2 ? nu : nu / Nf;
+  int lo = 0, len = N;
+  while (true) {
+    // chunk l = [l*step, min((l+1)*step, len)) of [lo, lo+len): its last bin
+    // below the key means the whole chunk is (bins are monotone)
+    const int step = (len + 63) >> 6;
+    const bool valid = lane * step < len;
+    const float b = valid ? bins[lo + min((lane + 1) * step, len) - 1] : 0.f;
+    const bool less = valid && (pow2 ? (b * Nf < key) : (b < key));
+    const int c = __popcll(__ballot(less));
+    if (step == 1) return min(lo + c, N - 1);
+    if (c * step >= len) return min(lo + len, N - 1);
+    lo += c * step;
+    len = min(step, len - c * step);
+  }
+}
 
 // end-of-temper bookkeeping, thread 0 of each tile: the iteration at which the
 // tile reached temperature 1, and (last tile, by ticket) the number of tiles
@@ -366,8 +400,17 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
       // a.ess[t] keeps the ESS of the tile's last step, as a single-tile
       // run of the reference reports it after its final resample
     }
-    if (a.flags & kDoResample)
-      for (int i = threadIdx.x; i < N; i += NT) a.idx[(size_t)t * N + i] = i;
+    if (a.flags & kDoResample) {
+      if (a.bins_out && a.method == SMCDET_RESAMPLE_SYSTEMATIC) {
+        // identity ancestors as bins: bins[i] = (i + 1)/N with U = 1/2 gives
+        // #{i : bins[i] < (n + 1/2)/N} = n exactly (bins_ancestor's test)
+        for (int i = threadIdx.x; i < N; i += NT)
+          a.bins_out[(size_t)t * N + i] = (float)(i + 1) / (float)N;
+        if (threadIdx.x == 0) a.bins_out[(size_t)a.T * N + t] = 0.5f;
+      } else {
+        for (int i = threadIdx.x; i < N; i += NT) a.idx[(size_t)t * N + i] = i;
+      }
+    }
     return;
   }
   TileLL<NT, PER> ll;
@@ -556,6 +599,20 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
                                 kTagResample, a.k0, a.k1);
         U = u01(r.x);
       }
+    }
+    if (a.bins_out && a.method == SMCDET_RESAMPLE_SYSTEMATIC) {
+      // the next sweep's waves search their own ancestors (bins_ancestor):
+      // hand over the bins and U instead of the indices
+      float* bo = a.bins_out + (size_t)t * N;
+      if ((N & 3) == 0) {
+        for (int i = 4 * (int)threadIdx.x; i < N; i += 4 * NT)
+          *reinterpret_cast<float4*>(bo + i) = *reinterpret_cast<const float4*>(buf + i);
+      } else {
+        for (int i = threadIdx.x; i < N; i += NT) bo[i] = buf[i];
+      }
+      if (threadIdx.x == 0) a.bins_out[(size_t)a.T * N + t] = U;
+      SMC_TRACE(trow, 6);
+      return;
     }
     const float total = buf[N - 1];
     int64_t* idxg = a.idx + (size_t)t * N;

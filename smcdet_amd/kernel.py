@@ -142,7 +142,14 @@ class SingleComponentMH(object):
         fluxes_out = torch.empty_like(fluxes)
         counts_out = None
         anc_p = None
-        if ancestors is not None:
+        if isinstance(ancestors, _hip.AncestorBins):
+            # the previous tile pass's bins: each wave of the sweep finds its
+            # own ancestor (the fused step's tail carries the buffer)
+            if tail is None:
+                raise ValueError("AncestorBins ancestors need the fused SMC step (tail)")
+            counts_out = torch.empty_like(counts)
+            tail.anc_bins = _hip.ptr(ancestors.buf)
+        elif ancestors is not None:
             ancestors = ancestors.to(device=dev, dtype=torch.int64).contiguous()
             counts_out = torch.empty_like(counts)
             anc_p = _hip.ptr(ancestors)

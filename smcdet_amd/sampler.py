@@ -260,7 +260,8 @@ class SMCsampler(object):
 
     def resample(self):
         """sampler.py:127-169."""
-        idx = self._pending_idx if self._pending_idx is not None else self.resample_index()
+        idx = (_hip.as_index(self._pending_idx) if self._pending_idx is not None
+               else self.resample_index())
         self._pending_idx = None
         self._gather(idx)
 
@@ -304,12 +305,13 @@ class SMCsampler(object):
             self.counts = self.MutationKernel.last_counts
         self._fresh_loglik = self.MutationKernel.last_loglik
 
-    def _tr_prepare(self, with_resample):
+    def _tr_prepare(self, with_resample, bins=False):
         """Output buffers of the temper / reweight (/ next resampling indices)
         pass, shared by its own launch (_temper_reweight) and the fused step
         (_step).  temperature / log Z are updated in place by the kernel (no
         per-step device copies); temperature_prev is a second persistent
-        buffer."""
+        buffer.  bins: the next resampling as AncestorBins (the step's tail
+        hands the bins to the next sweep, which searches the ancestors)."""
         new_t = self.temperature
         shape = tuple(self.counts.shape)
         prev_t = getattr(self, "temperature_prev", None)
@@ -324,7 +326,9 @@ class SMCsampler(object):
         # ESS of its last step)
         live = self._live_ws()
         idx = None
-        if with_resample:
+        if with_resample and bins:
+            idx = _hip.AncestorBins.empty(shape, new_t.device)
+        elif with_resample:
             idx = torch.empty(shape, device=new_t.device, dtype=torch.int64)
         return prev_t, live, idx
 
@@ -351,6 +355,12 @@ class SMCsampler(object):
             _hip.ptr(getattr(self, "_go", None)), getattr(self, "_live_host", None),
             _hip.stream_of(new_t)), "smcdet_temper_reweight")
         self._tr_finish(prev_t, live, idx)
+
+    # True (systematic resampling): the step's tile pass hands the next
+    # resampling to the next sweep as bins + offset (AncestorBins), whose
+    # waves search their own ancestors -- the tile pass skips the index search
+    # (DESIGN.md §4.2); False: int64 indices, as smcdet_temper_reweight writes
+    ancestor_bins = True
 
     # True: SMC iterations run as one launch (smcdet_mh_sweep_step: the MH
     # sweep's last workgroup per tile tempers, reweights and draws the next
@@ -387,7 +397,8 @@ class SMCsampler(object):
             self._temper_reweight(with_resample=True)
             return
         N = self.counts.shape[-1]
-        prev_t, live, idx_next = self._tr_prepare(True)
+        use_bins = self.ancestor_bins and self.resample_method == "systematic"
+        prev_t, live, idx_next = self._tr_prepare(True, bins=use_bins)
         tail = _hip.SmcTailC()
         tail.temperature_prev = _hip.ptr(prev_t)
         tail.log_weights_unnorm = _hip.ptr(self.weights_log_unnorm)
@@ -399,7 +410,10 @@ class SMCsampler(object):
         tail.flags = ((_hip.SMCDET_SMC_FREEZE_DONE if self.stopping == "independent" else 0)
                       | (0 if self.fused_step else _hip.SMCDET_SMC_TWO_LAUNCH))
         tail.seed = self.rng.seed
-        tail.idx = _hip.ptr(idx_next)
+        if use_bins:
+            tail.bins_out = _hip.ptr(idx_next.buf)
+        else:
+            tail.idx = _hip.ptr(idx_next)
         ru = None
         if resample_u is not None:
             ru = _hip.dev_f32(torch.as_tensor(resample_u, device=self.device,
@@ -668,6 +682,8 @@ class SMCsampler(object):
         as the uninterrupted one; without them the next sweep re-renders."""
         st = {k: getattr(self, k).clone() for k in self._CKPT_TENSORS
               if torch.is_tensor(getattr(self, k, None))}
+        if isinstance(getattr(self, "_pending_idx", None), _hip.AncestorBins):
+            st["_pending_idx"] = self._pending_idx.to_index()
         st["iter"] = int(getattr(self, "iter", 0))
         st["rng"] = self.rng.state()
         if with_rate_images and self._rate_valid and self._rate[self._rate_cur] is not None:

@@ -42,7 +42,8 @@ def _state(s):
             "weights_log_unnorm", "locs", "fluxes", "counts", "loglik")
     out = {k: getattr(s, k).detach().cpu().numpy().copy() for k in keys}
     if s._pending_idx is not None:
-        out["idx"] = s._pending_idx.cpu().numpy().copy()
+        from smcdet_amd import _hip
+        out["idx"] = _hip.as_index(s._pending_idx).cpu().numpy().copy()
     return out
 
 
@@ -133,3 +134,52 @@ def test_launch_timing_on_dispatch_events():
         _hip.launch_timing(0)
     assert len(ms) == 2 and all(0.0 < x < 1000.0 for x in ms)
     _assert_same(ta, _steps(b, 3))
+
+
+@pytest.mark.parametrize("stopping", ["lockstep", "independent"])
+def test_ancestor_bins_equal_indices(stopping):
+    """The step's tile pass hands the next systematic resampling to the next
+    sweep as bins + offset (AncestorBins, ABI 16), whose waves search their
+    own ancestors: the same indices and the same run, bit for bit, as the
+    int64 index hand-over (SMCsampler.ancestor_bins = False)."""
+    from smcdet_amd.sampler import SMCsampler
+    out = []
+    for bins in (True, False):
+        torch.manual_seed(3)
+        H, N = 32, 1024
+        s = SMCsampler(_image(H, 5), H, p_m71_prior(H, 10, 10, counts_rate=0.003125),
+                       p_m71_model(H), p_m71_mh(30), N, 0.5, "systematic",
+                       M71["flux_detection_threshold"], 200, print_every=10 ** 9, seed=21,
+                       device=DEV, stopping=stopping)
+        s.ancestor_bins = bins
+        s.run()
+        torch.cuda.synchronize()
+        out.append({k: getattr(s, k).detach().cpu().numpy().copy()
+                    for k in ("temperature", "log_normalizing_constant", "ess", "locs", "fluxes",
+                              "counts", "weights")} | {"iter": np.array(s.iter)})
+    assert out[0]["iter"] >= 5
+    for k in out[0]:
+        np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)
+
+
+@pytest.mark.parametrize("N", [4096, 1000, 7, 64, 65, 16384])
+def test_bins_index_vs_oracle(N):
+    """smcdet_bins_index (the sweep's 64-ary ancestor search) against the
+    oracle's bucketize of the same weights and offsets: random, degenerate
+    (one particle, a block of zero weights) and uniform weights."""
+    from oracle import smc_oracle as O
+    from smcdet_amd import _hip
+    rng = np.random.default_rng(N)
+    W = np.stack([rng.random(N), np.eye(1, N, rng.integers(N))[0],
+                  np.where(np.arange(N) % 7 < 3, 0.0, rng.random(N)), np.ones(N)])
+    W = (W / W.sum(1, keepdims=True)).astype(np.float32)
+    T = W.shape[0]
+    U = rng.random(T).astype(np.float32)
+    U[-1] = 0.0  # an offset of exactly 0
+    bins = np.cumsum(W.astype(np.float64), axis=1).astype(np.float32)  # the tile pass's bins
+    buf = torch.tensor(np.concatenate([bins.ravel(), U]), device=DEV)
+    idx = torch.empty(T, N, device=DEV, dtype=torch.int64)
+    _hip.check(_hip.lib().smcdet_bins_index(_hip.ptr(buf), T, N, _hip.ptr(idx),
+                                            _hip.stream_of(idx)), "bins_index")
+    ref = O.systematic_resample_index(W.reshape(1, T, N), U.reshape(1, T)).reshape(T, N)
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref)
