@@ -152,6 +152,9 @@ def parse():
     # A/B: the temper/reweight/resample pass inside the sweep's launch
     # (SMCsampler.fused_step) instead of the default two back-to-back launches
     ap.add_argument("--fused-step", action="store_true")
+    # A/B: the tile pass writes int64 resampling indices instead of handing
+    # bins to the next sweep (SMCsampler.ancestor_bins = False)
+    ap.add_argument("--ancestor-indices", action="store_true")
     # no kernel-timing pass after the timed region (the roofline then uses the
     # step time as the kernel time)
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -803,7 +806,9 @@ def main():
         return
     s, mh, steps_per_step, cpu_tile, cfg = build_sampler(args, dev, rank)
     s.fused_step = args.fused_step
+    s.ancestor_bins = not args.ancestor_indices
     s.initialize()
+    cfg = dict(cfg, ancestors="indices" if args.ancestor_indices else "bins")
     cfg = dict(cfg, step="two launches" if not args.fused_step else (
         "fused" if s._step_fusable() and _hip_fused(s) else "two launches (shape)"))
     s._temper_reweight(with_resample=True)

@@ -21,7 +21,7 @@ from smcdet_amd import _hip  # noqa: E402
 from smcdet_amd.sampler import SMCsampler  # noqa: E402
 
 MH_PHASES = ["stage image", "state + tn caches", "initial render", "MH loop", "write back"]
-TILE_PHASES = ["load ll + max", "f(top)", "brentq", "weights", "cumsum", "index search + store"]
+TILE_PHASES = ["load ll + max", "f(top)", "brentq", "weights", "cumsum", "bins store (or index search)"]
 
 
 def read(name, cols):

@@ -7,6 +7,7 @@ or the tensors are not float32 CUDA(HIP) tensors, the call raises.
 from __future__ import annotations
 
 import ctypes
+import functools
 import os
 
 import torch
@@ -266,6 +267,32 @@ SOURCES = tuple(os.path.join(_REPO, p) for p in (
     "smcdet_amd/csrc/chain_kernel.hip", "smcdet_amd/csrc/smc_kernels.hip",
     "smcdet_amd/csrc/agg_kernel.hip", "smcdet_amd/csrc/device.h", "smcdet_amd/csrc/render.h",
     "smcdet_amd/csrc/mcmc.h", "smcdet_amd/csrc/tile.h", "include/smcdet_hip.h"))
+
+
+def cached_struct(build):
+    """Memoises a per-object C struct builder (`_cmodel`, `_cprior`): the
+    struct is rebuilt only when one of the object's instance attributes is
+    rebound (keyed on the attributes' identities; the cache keeps those
+    objects alive, so an identity cannot be reused).  The tensors and lists
+    the builders read are treated as read-only, as the reference does.  Saves
+    the per-call float conversions on the sampler's per-step host path.  The
+    struct is shared: a caller that changes a field works on a copy
+    (`type(c).from_buffer_copy(c)`)."""
+    slot = "_cs_" + build.__qualname__
+    if os.environ.get("SMCDET_NO_STRUCT_CACHE"):  # (diagnostic: rebuild on every call)
+        return build
+
+    @functools.wraps(build)
+    def wrapper(self):
+        vals = tuple(v for k, v in vars(self).items() if not k.startswith("_cs_"))
+        key = tuple(map(id, vals))
+        hit = self.__dict__.get(slot)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        c = build(self)
+        self.__dict__[slot] = (key, c, vals)
+        return c
+    return wrapper
 
 
 def source_hash():

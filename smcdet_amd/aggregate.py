@@ -175,6 +175,8 @@ def aggregate_sweep(image_model, prior, mh, axis, data, temperature, counts, loc
     dev = locs.device
     ch = mh._cmh(prior)
     if num_iters is not None:
+        # (a copy: _cmh returns the kernel's cached struct)
+        ch = _hip.MHC.from_buffer_copy(ch)
         ch.num_iters = int(num_iters)
     co, lo, lf = torch.empty_like(counts), torch.empty_like(locs), torch.empty_like(fluxes)
     lp = torch.empty(nH, nW, N, device=dev)

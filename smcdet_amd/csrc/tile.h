@@ -23,6 +23,8 @@
 
 #include <math.h>
 
+#include <type_traits>
+
 #include "device.h"
 
 namespace smcdet {
@@ -142,8 +144,37 @@ __device__ __forceinline__ int vwave(int h) {
 }
 
 // Workgroup reductions with ONE barrier each: wave DPP reductions per virtual
-// wave -> its slot -> every thread combines the kTW slots in a fixed order
-// (deterministic; every thread ends with the same value).
+// wave -> its slot -> the kTW slots combined in a fixed order (deterministic;
+// every thread ends with the same value).
+//
+// The combine: lane i < 8 of every wave reads slot i of the first sum, lane
+// 8 + i slot i of the second, one LDS read per lane, then a pairwise tree over
+// the 8 lanes (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror: lane 0 ends
+// with ((s0+s1)+(s2+s3))+((s4+s5)+(s6+s7)), lane 8 likewise), read back with
+// v_readlane.  Every thread reading every slot instead moved 16-64 KB through
+// the LDS return path per reduction at 512 threads (~130-500 cycles on the
+// Brent path: scripts/probe/brent_probe.hip).
+static_assert(kTW == 8, "the slot combine is an 8-lane tree");
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ void slot_tree2(float v, float& A, float& B) {
+  v += dpp_f<0xb1>(v);
+  v += dpp_f<0x4e>(v);
+  v += dpp_f<0x141>(v);
+  A = readlane(v, 0);
+  B = readlane(v, 8);
+}
+__device__ __forceinline__ void slot_tree2(double v, double& A, double& B) {
+  v += dpp_d<0xb1>(v);
+  v += dpp_d<0x4e>(v);
+  v += dpp_d<0x141>(v);
+  A = readlane_d(v, 0);
+  B = readlane_d(v, 8);
+}
 template <int NT>
 __device__ __forceinline__ double vblock_sumd(const double (&a)[VLayout<NT>::VPT], TileRed* r,
                                               int& parity) {
@@ -156,9 +187,8 @@ __device__ __forceinline__ double vblock_sumd(const double (&a)[VLayout<NT>::VPT
     if (lane == 0) r->d[k][vwave<NT>(h)][0] = s;
   }
   __syncthreads();
-  double sa = 0.0;
-#pragma unroll
-  for (int i = 0; i < kTW; ++i) sa += r->d[k][i][0];
+  double sa, sb;
+  slot_tree2(r->d[k][lane & 7][0], sa, sb);
   return sa;
 }
 template <int NT>
@@ -178,14 +208,7 @@ __device__ __forceinline__ void vblock_sum2d(const double (&a)[VLayout<NT>::VPT]
     }
   }
   __syncthreads();
-  double sa = 0.0, sb = 0.0;
-#pragma unroll
-  for (int i = 0; i < kTW; ++i) {
-    sa += r->d[k][i][0];
-    sb += r->d[k][i][1];
-  }
-  A = sa;
-  B = sb;
+  slot_tree2(r->d[k][lane & 7][(lane >> 3) & 1], A, B);
 }
 template <int NT>
 __device__ __forceinline__ void vblock_sum2f(const float (&a)[VLayout<NT>::VPT],
@@ -204,22 +227,7 @@ __device__ __forceinline__ void vblock_sum2f(const float (&a)[VLayout<NT>::VPT],
     }
   }
   __syncthreads();
-  float sa[kTW], sb[kTW];
-#pragma unroll
-  for (int i = 0; i < kTW; ++i) {
-    sa[i] = r->f2[k][i][0];
-    sb[i] = r->f2[k][i][1];
-  }
-#pragma unroll
-  for (int w = 1; w < kTW; w <<= 1) {
-#pragma unroll
-    for (int i = 0; i + w < kTW; i += 2 * w) {
-      sa[i] += sa[i + w];
-      sb[i] += sb[i + w];
-    }
-  }
-  A = sa[0];
-  B = sb[0];
+  slot_tree2(r->f2[k][lane & 7][(lane >> 3) & 1], A, B);
 }
 template <int NT>
 __device__ __forceinline__ float vblock_max(const float (&v)[VLayout<NT>::VPT], TileRed* r,
@@ -233,10 +241,11 @@ __device__ __forceinline__ float vblock_max(const float (&v)[VLayout<NT>::VPT], 
     if (lane == 0) r->f[k][vwave<NT>(h)] = m;
   }
   __syncthreads();
-  float m = -INFINITY;
-#pragma unroll
-  for (int i = 0; i < kTW; ++i) m = fmaxf(m, r->f[k][i]);
-  return m;
+  float m = r->f[k][lane & 7];
+  m = fmaxf(m, dpp_fmax<0xb1>(m));
+  m = fmaxf(m, dpp_fmax<0x4e>(m));
+  m = fmaxf(m, dpp_fmax<0x141>(m));
+  return readlane(m, 0);
 }
 
 // the 512-thread forms (aggregation kernels)
@@ -292,27 +301,57 @@ struct TileLL {
 // the reference's own float32 logsumexp level); only the ratio is double.
 // This sits on the latency-bound path of every Brent iteration, so it is
 // short: one exp per element, float DPP reductions, one barrier.
+//
+// In gfx950's packed float ops: element j is paired with element j + PER/2
+// (v_pk_mul / v_pk_add: the same roundings per element), the pairs summed by
+// a pairwise tree and the two halves added last -- for PER a power of two
+// exactly tree_sum's order over the PER elements.  Tiles of exactly kTB * PER
+// particles skip the per-element bounds masks.
 template <int NT, int PER>
-__device__ __forceinline__ double block_ess_objective(const TileLL<NT, PER>& ll, int N, float lmax,
-                                                      double delta, double thr, TileRed* red,
-                                                      int& parity) {
+__device__ __forceinline__ double block_ess_objective(const TileLL<NT, PER>& ll, int N,
+                                                      float lmax, double delta, double thr,
+                                                      TileRed* red, int& parity) {
 #pragma clang fp contract(off)
   constexpr int VPT = VLayout<NT>::VPT;
   const float df = (float)delta;
-  const float m = df * lmax;  // = max_i fl(df*l_i): rounding is monotone
+  const float m = df * lmax;
   float s1[VPT], s2[VPT];
+  auto sums = [&](auto full) {
 #pragma unroll
-  for (int h = 0; h < VPT; ++h) {
-    float e1[PER], e2[PER];
+    for (int h = 0; h < VPT; ++h) {
+      if constexpr (PER % 2 == 0) {
+        constexpr int H = PER / 2;
+        f2 E[H], Q[H];
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const float e = ll.valid(h, j, N) ? fast_exp2((df * ll.l[h][j] - m) * kLog2e) : 0.f;
-      e1[j] = e;
-      e2[j] = e * e;
+        for (int k = 0; k < H; ++k) {
+          f2 v = f2{ll.l[h][k], ll.l[h][k + H]} * df;
+          v = (v - m) * kLog2e;
+          f2 e = exp2_2(v);
+          if constexpr (!decltype(full)::value) {
+            e.x = ll.valid(h, k, N) ? e.x : 0.f;
+            e.y = ll.valid(h, k + H, N) ? e.y : 0.f;
+          }
+          E[k] = e;
+          Q[k] = e * e;
+        }
+        const f2 se = tree_sum(E), sq = tree_sum(Q);
+        s1[h] = se.x + se.y;
+        s2[h] = sq.x + sq.y;
+      } else {
+        float e1[PER], e2[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+          const float e = ll.valid(h, j, N) ? fast_exp2((df * ll.l[h][j] - m) * kLog2e) : 0.f;
+          e1[j] = e;
+          e2[j] = e * e;
+        }
+        s1[h] = tree_sum(e1);
+        s2[h] = tree_sum(e2);
+      }
     }
-    s1[h] = tree_sum(e1);
-    s2[h] = tree_sum(e2);
-  }
+  };
+  if (N == kTB * PER) sums(std::true_type{});
+  else sums(std::false_type{});
   float S1, S2;
   vblock_sum2f<NT>(s1, s2, S1, S2, red, parity);
   const double d1 = (double)S1;
@@ -322,7 +361,10 @@ __device__ __forceinline__ double block_ess_objective(const TileLL<NT, PER>& ll,
 // scipy.optimize.brentq (scipy/optimize/Zeros/brentq.c, the algorithm the
 // reference calls at sampler.py:114-120) with xtol = rtol = 1e-6, maxiter
 // 100.  Every thread runs the (deterministic) control flow on identical
-// values; the workgroup evaluates f together.
+// values; the workgroup evaluates f together.  (brentq.c's branches stay
+// branches: a select form computing every candidate step measured 745-787
+// vs 644-675 cycles of control per iteration, round 4's
+// scripts/probe/brent_probe.hip, as in round 2.)
 template <class F>
 __device__ double block_brentq(F&& f, double xa, double xb, double fa, double fb) {
 #pragma clang fp contract(off)

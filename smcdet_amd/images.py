@@ -53,6 +53,7 @@ class ImageModel(object):
         read image_height / image_width on every call: nothing to update."""
 
     # -- C-ABI description -------------------------------------------------
+    @_hip.cached_struct
     def _cmodel(self):
         if self.psf_stdev is None:
             raise NotImplementedError("ImageModel needs psf_stdev for the HIP path")
@@ -164,6 +165,7 @@ class M71ImageModel(ImageModel):
     def _compute_normalized_psf(self, r):
         return self._compute_unnormalized_psf(r) / self.psf_normalizing_constant.to(r.device)
 
+    @_hip.cached_struct
     def _cmodel(self):
         c = _hip.ImageModelC()
         c.model = _hip.SMCDET_MODEL_M71

@@ -61,6 +61,25 @@ class SingleComponentMH(object):
         return prior, image_model
 
     def _cmh(self, prior):
+        """The smcdet_mh_params_t of this kernel, rebuilt only when a parameter
+        attribute is rebound (the reference's SMCsampler assigns locs_min /
+        locs_max once; every tensor parameter is read-only), so the per-step
+        host path skips its tensor -> float conversions.  The struct is shared:
+        a caller that changes a field works on a copy (from_buffer_copy)."""
+        key = (id(prior), self.num_iters, id(self.locs_stdev), id(self.fluxes_stdev),
+               id(self.fluxes_min), id(self.fluxes_max), id(self.locs_min), id(self.locs_max),
+               id(prior.loc_prior.low), id(prior.loc_prior.high))
+        hit = getattr(self, "_cmh_cached", None)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        c = self._cmh_build(prior)
+        # (the key's objects are kept alive with it, so their ids stay theirs)
+        self._cmh_cached = (key, c, (prior, self.locs_stdev, self.fluxes_stdev, self.fluxes_min,
+                                     self.fluxes_max, self.locs_min, self.locs_max,
+                                     prior.loc_prior.low, prior.loc_prior.high))
+        return c
+
+    def _cmh_build(self, prior):
         c = _hip.MHC()
         c.num_iters = int(self.num_iters)
         c.locs_stdev = _f32(self.locs_stdev)

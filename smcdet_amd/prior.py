@@ -107,6 +107,7 @@ class PointProcessPrior(object):
                           dtype=torch.float64)
 
     # --- C-ABI description ----------------------------------------------------
+    @_hip.cached_struct
     def _cprior(self):
         raise NotImplementedError(
             f"{type(self).__name__} has no flux prior; the HIP path supports M71Prior and "
@@ -246,6 +247,7 @@ class ParetoStarPrior(PointProcessPrior):
         u = torch.rand(*shape, device=device)
         return _f32(self.flux_scale) * (1.0 - u) ** (-1.0 / _f32(self.flux_alpha))
 
+    @_hip.cached_struct
     def _cprior(self):
         c = self._fill_common(_hip.PriorC())
         c.kind = _hip.SMCDET_PRIOR_PARETO
@@ -273,6 +275,7 @@ class M71Prior(PoissonProcessPrior):
         counts = torch.arange(self.min_objects, self.max_objects + 1)[k]
         return counts.to(device=device, dtype=torch.float32)
 
+    @_hip.cached_struct
     def _cprior(self):
         c = self._fill_common(_hip.PriorC())
         c.kind = _hip.SMCDET_PRIOR_M71

@@ -245,6 +245,7 @@ class SMCsampler(object):
         return idx
 
     def _gather(self, idx):
+        idx = _hip.as_index(idx)  # (AncestorBins from a fused step: searched first)
         N = idx.shape[-1]
         S = self.locs.shape[-2]
         c, l, f = (torch.empty_like(self.counts), torch.empty_like(self.locs),
@@ -260,8 +261,7 @@ class SMCsampler(object):
 
     def resample(self):
         """sampler.py:127-169."""
-        idx = (_hip.as_index(self._pending_idx) if self._pending_idx is not None
-               else self.resample_index())
+        idx = self._pending_idx if self._pending_idx is not None else self.resample_index()
         self._pending_idx = None
         self._gather(idx)
 

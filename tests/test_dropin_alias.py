@@ -105,3 +105,35 @@ def test_unsupported_shapes_fail_at_construction():
     model, prior = make(32, 10)
     with pytest.raises(ValueError, match="20000 particles per tile > 16384"):
         SMCsampler(torch.zeros(32, 32), 32, prior, model, mh, 20000, 0.5, "systematic", 0.25, 10)
+
+
+def test_struct_caches_follow_rebinding():
+    """_cmh / _cmodel / _cprior are cached per object (the per-step host
+    path) and rebuilt when a parameter attribute is rebound; the struct is
+    shared, so Aggregate's num_iters override works on a copy."""
+    from smcdet_amd import _hip
+    from smcdet_amd.images import M71ImageModel
+    from smcdet_amd.kernel import SingleComponentMH
+    from tests._params import p_m71_model, p_m71_prior
+    k = SingleComponentMH(100, 0.1, 2.5, 0.06, 1800.0)
+    prior = p_m71_prior(16, 0, 4)
+    c1 = k._cmh(prior)
+    assert k._cmh(prior) is c1
+    k.locs_stdev = torch.tensor(0.2)
+    c2 = k._cmh(prior)
+    assert c2 is not c1 and c2.locs_stdev == pytest.approx(0.2)
+    k.num_iters = 7
+    assert k._cmh(prior).num_iters == 7
+    cp = _hip.MHC.from_buffer_copy(k._cmh(prior))
+    cp.num_iters = 0
+    assert k._cmh(prior).num_iters == 7
+    model = p_m71_model(16)
+    assert isinstance(model, M71ImageModel)
+    m1 = model._cmodel()
+    assert model._cmodel() is m1 and m1.H == 16
+    model.image_height = 32
+    assert model._cmodel().H == 32
+    p1 = prior._cprior()
+    assert prior._cprior() is p1
+    prior.max_objects = 9
+    assert prior._cprior().max_objects == 9
