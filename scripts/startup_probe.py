@@ -1,9 +1,10 @@
 #!/usr/bin/env python
 """Fixed cost of a timed region (C2): bench.py times K steps between two
-synchronisations, so ms_per_step = GPU step + C/K.  Measures the wall time
-of K = 1..40 back-to-back SMC steps, the host time to enqueue the first step
-after a synchronisation, and an idle synchronisation, to split C into host
-enqueue and the rest."""
+synchronisations, so ms_per_step = GPU step + C/K.  For K = 20 steps:
+the wall time, the GPU time per back-to-back step (events after step 1 and
+after step K), the delay before step 1's kernels start (host enqueue after an
+idle GPU), and the rest (the host noticing completion) -- with
+torch.cuda.synchronize() alone and after spinning on an event query."""
 import json
 import os
 import sys
@@ -12,7 +13,6 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import bench  # noqa: E402
@@ -39,26 +39,44 @@ def main():
     for _ in range(3):
         step()
     torch.cuda.synchronize()
-    out = {"wall_ms": {}, "first_enqueue_us": [], "idle_sync_us": []}
-    for k in (1, 2, 5, 10, 20, 40, 1, 2, 5, 10, 20, 40):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        step()
-        t1 = time.perf_counter()
-        for _ in range(k - 1):
+    out = {"rows": []}
+    main_stream = torch.cuda.current_stream(dev)
+
+    def spin():
+        ev = torch.cuda.Event()
+        ev.record(main_stream)
+        while not ev.query():
+            pass
+
+    for rep in range(4):
+        for mode in ("sync", "spin"):
+            k = 20
+            torch.cuda.synchronize()
+            e0, e0b, e1 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            t0 = time.perf_counter()
+            e0.record(main_stream)
             step()
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        out["wall_ms"].setdefault(k, []).append((t2 - t0) * 1e3)
-        out["first_enqueue_us"].append((t1 - t0) * 1e6)
-        a = time.perf_counter()
-        torch.cuda.synchronize()
-        out["idle_sync_us"].append((time.perf_counter() - a) * 1e6)
-        print(k, round((t2 - t0) * 1e3 / k, 4), "ms/step", flush=True)
-    ks = np.array(sorted(out["wall_ms"]), dtype=np.float64)
-    w = np.array([min(out["wall_ms"][int(k)]) for k in ks])
-    slope, icpt = np.polyfit(ks, w, 1)
-    out["fit"] = {"gpu_ms_per_step": slope, "fixed_ms": icpt}
+            e0b.record(main_stream)
+            t1 = time.perf_counter()
+            for _ in range(k - 1):
+                step()
+            e1.record(main_stream)
+            if mode == "spin":
+                spin()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            gpu = e0.elapsed_time(e1)
+            g = e0b.elapsed_time(e1) / (k - 1)  # back-to-back steps: GPU time per step
+            row = dict(mode=mode, k=k, wall_ms=(t2 - t0) * 1e3, event_ms=gpu, gpu_step_ms=g,
+                       wall_minus_k_steps_us=((t2 - t0) * 1e3 - k * g) * 1e3,
+                       first_step_start_delay_us=(e0.elapsed_time(e0b) - g) * 1e3,
+                       wall_minus_event_us=((t2 - t0) * 1e3 - gpu) * 1e3,
+                       first_enqueue_us=(t1 - t0) * 1e6)
+            out["rows"].append(row)
+            print(json.dumps(row), flush=True)
+    a = time.perf_counter()
+    torch.cuda.synchronize()
+    out["idle_sync_us"] = (time.perf_counter() - a) * 1e6
     print(json.dumps(out))
 
 

@@ -607,6 +607,12 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
       if (lane == 63) red.d[k][vwave<NT>(h)][0] = incl[h];
     __syncthreads();
     SMC_TRACE(trow, 5);
+    // systematic resampling handed to the next sweep (bins_ancestor): the
+    // bins go straight to bins_out (coalesced: thread chunks are adjacent),
+    // not through LDS
+    const bool to_bins = a.bins_out && a.method == SMCDET_RESAMPLE_SYSTEMATIC;
+    float* dst = to_bins ? a.bins_out + (size_t)t * N : buf;
+    const bool dst_al16 = ((uintptr_t)dst & 15) == 0;  // (a C caller's bins_out may not be)
 #pragma unroll
     for (int h = 0; h < VPT; ++h) {
       double base = 0.0;
@@ -619,19 +625,24 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
             run += (double)cv[h][i];
             cv[h][i] = (float)run;
           }
-          *reinterpret_cast<float4*>(buf + b0[h]) =
-              make_float4(cv[h][0], cv[h][1], cv[h][2], cv[h][3]);
-          *reinterpret_cast<float4*>(buf + b0[h] + 4) =
-              make_float4(cv[h][4], cv[h][5], cv[h][6], cv[h][7]);
+          if (dst_al16) {
+            *reinterpret_cast<float4*>(dst + b0[h]) =
+                make_float4(cv[h][0], cv[h][1], cv[h][2], cv[h][3]);
+            *reinterpret_cast<float4*>(dst + b0[h] + 4) =
+                make_float4(cv[h][4], cv[h][5], cv[h][6], cv[h][7]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dst[b0[h] + i] = cv[h][i];
+          }
         }
       } else {
         for (int i = b0[h]; i < b1[h]; ++i) {
           run += (double)buf[i];
-          buf[i] = (float)run;
+          dst[i] = (float)run;
         }
       }
     }
-    __syncthreads();
+    if (!to_bins) __syncthreads();
     float U = 0.f;
     if (a.method == SMCDET_RESAMPLE_SYSTEMATIC) {
       if (a.u) {
@@ -642,16 +653,9 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
         U = u01(r.x);
       }
     }
-    if (a.bins_out && a.method == SMCDET_RESAMPLE_SYSTEMATIC) {
+    if (to_bins) {
       // the next sweep's waves search their own ancestors (bins_ancestor):
-      // hand over the bins and U instead of the indices
-      float* bo = a.bins_out + (size_t)t * N;
-      if ((N & 3) == 0) {
-        for (int i = 4 * (int)threadIdx.x; i < N; i += 4 * NT)
-          *reinterpret_cast<float4*>(bo + i) = *reinterpret_cast<const float4*>(buf + i);
-      } else {
-        for (int i = threadIdx.x; i < N; i += NT) bo[i] = buf[i];
-      }
+      // the bins (written above) and U instead of the indices
       if (threadIdx.x == 0) a.bins_out[(size_t)a.T * N + t] = U;
       SMC_TRACE(trow, 6);
       return;
