@@ -136,17 +136,19 @@ def test_launch_timing_on_dispatch_events():
     _assert_same(ta, _steps(b, 3))
 
 
-@pytest.mark.parametrize("stopping", ["lockstep", "independent"])
-def test_ancestor_bins_equal_indices(stopping):
+@pytest.mark.parametrize("stopping,N", [("lockstep", 1024), ("independent", 1024),
+                                        ("lockstep", 1000)])
+def test_ancestor_bins_equal_indices(stopping, N):
     """The step's tile pass hands the next systematic resampling to the next
     sweep as bins + offset (AncestorBins, ABI 16), whose waves search their
     own ancestors: the same indices and the same run, bit for bit, as the
-    int64 index hand-over (SMCsampler.ancestor_bins = False)."""
+    int64 index hand-over (SMCsampler.ancestor_bins = False); N = 1000: the
+    search's division form for N not a power of two."""
     from smcdet_amd.sampler import SMCsampler
     out = []
     for bins in (True, False):
         torch.manual_seed(3)
-        H, N = 32, 1024
+        H = 32
         s = SMCsampler(_image(H, 5), H, p_m71_prior(H, 10, 10, counts_rate=0.003125),
                        p_m71_model(H), p_m71_mh(30), N, 0.5, "systematic",
                        M71["flux_detection_threshold"], 200, print_every=10 ** 9, seed=21,
