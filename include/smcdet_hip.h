@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 16
+#define SMCDET_ABI_VERSION 17
 
 /* status codes */
 #define SMCDET_OK 0
@@ -390,12 +390,16 @@ typedef struct smcdet_smc_tail {
   int32_t iter;
   int32_t reserved;
   /* (ABI 16) systematic resampling handed to the next sweep as bins instead
-   * of indices: bins_out [T*N + T] (nullable) receives the tile's running sum
-   * of the new weights (float32 roundings of the float64 cumsum) followed by
-   * the T offsets U -- the tile pass then skips the index search; anc_bins
-   * (nullable, input) is such a buffer from the previous step, and each wave
-   * of this sweep finds its own ancestor in it (idx[n] = #{i : bins[i] <
-   * (n + U)/N}, clamped to N - 1: the same indices, bit for bit) in place of
+   * of indices: bins_out (nullable; SMCDET_BINS_FLOATS(T, N) floats) receives
+   * the tile's running sum of the new weights, [T*N] (float32 roundings of the
+   * float64 cumsum), then the T offsets U, then (ABI 17) per tile the 64
+   * chunk-end bins of the search's first level, [T*64]: entry l is
+   * bins[min((l+1)*c, N) - 1] for l < ceil(N/c), c = ceil(N/64) -- so the
+   * first level reads 256 contiguous bytes per wave instead of 64 strided
+   * lines.  The tile pass then skips the index search; anc_bins (nullable,
+   * input) is such a buffer from the previous step, and each wave of this
+   * sweep finds its own ancestor in it (idx[n] = #{i : bins[i] < (n + U)/N},
+   * clamped to N - 1: the same indices, bit for bit) in place of
    * `ancestors`.  smcdet_bins_index converts a buffer to the indices. */
   const float* anc_bins;
   float* bins_out;
@@ -430,8 +434,10 @@ int smcdet_mh_sweep_step_fused(const smcdet_image_model_t* model, int32_t N,
 
 /* Gather of the resampled state (smcdet/sampler.py:150-169). */
 /* The systematic resampling indices [T,N] of a bins buffer (the tail's
- * bins_out layout: [T*N] running sums, then [T] offsets U): idx[t,n] =
- * #{i : bins[t,i] < (n + U_t)/N} clamped to N - 1 (sampler.py:141-148). */
+ * bins_out layout: [T*N] running sums, [T] offsets U, [T*64] first-level
+ * chunk ends): idx[t,n] = #{i : bins[t,i] < (n + U_t)/N} clamped to N - 1
+ * (sampler.py:141-148). */
+#define SMCDET_BINS_FLOATS(T, N) ((size_t)(T) * (size_t)(N) + (size_t)(T) * 65u)
 int smcdet_bins_index(const float* bins, int32_t T, int32_t N, int64_t* idx, void* stream);
 
 int smcdet_gather(const int64_t* idx, int32_t T, int32_t N, int32_t S,

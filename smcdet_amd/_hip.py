@@ -24,7 +24,7 @@ SMCDET_RESAMPLE_SYSTEMATIC = 1
 SMCDET_MH_FULL_RECOMPUTE = 1
 SMCDET_MH_COMPONENT_BY_COUNT = 2
 SMCDET_MH_SKIP_DONE = 4
-ABI_VERSION = 16
+ABI_VERSION = 17
 SMCDET_SMC_FREEZE_DONE = 1
 SMCDET_SMC_TWO_LAUNCH = 2
 
@@ -414,11 +414,12 @@ def ref(x):
 
 class AncestorBins:
     """The next systematic resampling as the MH sweep reads it
-    (smcdet_smc_tail_t.anc_bins / bins_out, ABI 16): per tile the running
-    sum of the weights (float32) and the offset U, [T*N + T] float32 -- each
-    wave of the next sweep searches its own ancestor, so the tile pass skips
-    the index search.  to_index() gives the [numH, numW, N] int64 indices (the
-    same ones, bit for bit)."""
+    (smcdet_smc_tail_t.anc_bins / bins_out, ABI 16/17): per tile the running
+    sum of the weights (float32), then the T offsets U, then per tile the 64
+    chunk ends of the search's first level -- SMCDET_BINS_FLOATS(T, N) =
+    T*N + 65*T float32.  Each wave of the next sweep searches its own
+    ancestor, so the tile pass skips the index search.  to_index() gives the
+    [numH, numW, N] int64 indices (the same ones, bit for bit)."""
 
     def __init__(self, buf, shape):
         self.buf = buf
@@ -427,7 +428,7 @@ class AncestorBins:
     @staticmethod
     def empty(shape, device):
         nH, nW, N = shape
-        return AncestorBins(torch.empty(nH * nW * N + nH * nW, device=device,
+        return AncestorBins(torch.empty(nH * nW * (N + 65), device=device,
                                         dtype=torch.float32), shape)
 
     def to_index(self):

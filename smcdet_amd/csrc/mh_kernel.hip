@@ -389,7 +389,9 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   size_t src = a.ancestors ? (size_t)t * N + (size_t)a.ancestors[pid] : pid;
   if (a.anc_bins)  // the wave finds its ancestor in the previous tile pass's bins
     src = (size_t)t * N +
-          (size_t)bins_ancestor(a.anc_bins + (size_t)t * N, N, a.anc_bins[(size_t)a.T * N + t], n);
+          (size_t)bins_ancestor(a.anc_bins + (size_t)t * N,
+                                a.anc_bins + (size_t)a.T * (N + 1) + (size_t)t * kBinsCoarse, N,
+                                a.anc_bins[(size_t)a.T * N + t], n);
   if constexpr (GL) lam = a.rate_out + pid * (size_t)HWp;
   const float count = a.counts_in[src];
   if (a.counts_out && lane == 0) a.counts_out[pid] = count;

@@ -363,7 +363,8 @@ __global__ __launch_bounds__(256) void bins_index_kernel(const float* __restrict
   const int t = blockIdx.y;
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (n >= N) return;
-  const int a = bins_ancestor(bins + (size_t)t * N, N, bins[(size_t)T * N + t], n);
+  const float* coarse = bins + (size_t)T * (N + 1) + (size_t)t * kBinsCoarse;
+  const int a = bins_ancestor(bins + (size_t)t * N, coarse, N, bins[(size_t)T * N + t], n);
   if ((threadIdx.x & 63) == 0) idx[(size_t)t * N + n] = a;
 }
 

@@ -70,11 +70,16 @@ int launch_tile(const TileArgs& a, hipStream_t st);
 // The systematic ancestor of particle n, idx[n] = #{i : bins[i] < u_n}
 // clamped to N - 1, u_n = (n + U)/N in float32 (sampler.py:141-148), found by
 // the 64 lanes of a wave in the monotone bins (global memory, L2-resident): a
-// 64-ary search, log64(N) dependent loads (two at N = 4096).  The test is
-// the tile pass's (bins[i] < u_n, for N a power of two as b*N < fl(n + U),
-// exact), so the index is the one the tile pass's search would write.  Call
-// from converged code; the result is wave-uniform.
-__device__ __forceinline__ int bins_ancestor(const float* __restrict__ bins, int N, float U,
+// 64-ary search, log64(N) dependent loads (two at N = 4096).  The first level
+// reads the tile's 64 chunk ends from `coarse` (kBinsCoarse contiguous floats,
+// written by the tile pass: one 256-byte read instead of 64 cache lines per
+// wave) when it is given.  The test is the tile pass's (bins[i] < u_n, for N a
+// power of two as b*N < fl(n + U), exact), so the index is the one the tile
+// pass's search would write.  Call from converged code; the result is
+// wave-uniform.
+constexpr int kBinsCoarse = 64;
+__device__ __forceinline__ int bins_ancestor(const float* __restrict__ bins,
+                                             const float* __restrict__ coarse, int N, float U,
                                              int n) {
   const int lane = threadIdx.x & 63;
   const float Nf = (float)N;
@@ -82,12 +87,14 @@ __device__ __forceinline__ int bins_ancestor(const float* __restrict__ bins, int
   const float nu = (float)n + U;
   const float key = pow2 ? nu : nu / Nf;
   int lo = 0, len = N;
+  bool first = coarse != nullptr;
   while (true) {
     // chunk l = [l*step, min((l+1)*step, len)) of [lo, lo+len): its last bin
     // below the key means the whole chunk is (bins are monotone)
     const int step = (len + 63) >> 6;
     const bool valid = lane * step < len;
-    const float b = valid ? bins[lo + min((lane + 1) * step, len) - 1] : 0.f;
+    const float b = !valid ? 0.f : first ? coarse[lane] : bins[lo + min((lane + 1) * step, len) - 1];
+    first = false;
     const bool less = valid && (pow2 ? (b * Nf < key) : (b < key));
     const int c = __popcll(__ballot(less));
     if (step == 1) return min(lo + c, N - 1);
@@ -95,6 +102,12 @@ __device__ __forceinline__ int bins_ancestor(const float* __restrict__ bins, int
     lo += c * step;
     len = min(step, len - c * step);
   }
+}
+
+// the chunk-end index of coarse entry l: min((l+1)*c, N) - 1, c = ceil(N/64)
+__device__ __forceinline__ int bins_coarse_end(int l, int N) {
+  const int c = (N + kBinsCoarse - 1) / kBinsCoarse;
+  return min((l + 1) * c, N) - 1;
 }
 
 // end-of-temper bookkeeping, thread 0 of each tile: the iteration at which the
@@ -449,6 +462,9 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
         for (int i = threadIdx.x; i < N; i += NT)
           a.bins_out[(size_t)t * N + i] = (float)(i + 1) / (float)N;
         if (threadIdx.x == 0) a.bins_out[(size_t)a.T * N + t] = 0.5f;
+        if (threadIdx.x < kBinsCoarse)
+          a.bins_out[(size_t)a.T * (N + 1) + (size_t)t * kBinsCoarse + threadIdx.x] =
+              (float)(bins_coarse_end(threadIdx.x, N) + 1) / (float)N;
       } else {
         for (int i = threadIdx.x; i < N; i += NT) a.idx[(size_t)t * N + i] = i;
       }
@@ -613,6 +629,11 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
     const bool to_bins = a.bins_out && a.method == SMCDET_RESAMPLE_SYSTEMATIC;
     float* dst = to_bins ? a.bins_out + (size_t)t * N : buf;
     const bool dst_al16 = ((uintptr_t)dst & 15) == 0;  // (a C caller's bins_out may not be)
+    // the first search level's chunk ends (bins_ancestor): element gi of a
+    // thread's chunk is entry l's end when gi == bins_coarse_end(l)
+    float* coarse = to_bins ? a.bins_out + (size_t)a.T * (N + 1) + (size_t)t * kBinsCoarse
+                            : nullptr;
+    const int cstep = (N + kBinsCoarse - 1) / kBinsCoarse;
 #pragma unroll
     for (int h = 0; h < VPT; ++h) {
       double base = 0.0;
@@ -625,6 +646,15 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
             run += (double)cv[h][i];
             cv[h][i] = (float)run;
           }
+          if (coarse) {
+            int l = b0[h] / cstep, end = bins_coarse_end(l, N);
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+              if (b0[h] + i == end) {
+                coarse[l] = cv[h][i];
+                end = bins_coarse_end(++l, N);
+              }
+          }
           if (dst_al16) {
             *reinterpret_cast<float4*>(dst + b0[h]) =
                 make_float4(cv[h][0], cv[h][1], cv[h][2], cv[h][3]);
@@ -636,9 +666,14 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
           }
         }
       } else {
+        int l = b0[h] / cstep, end = bins_coarse_end(l, N);
         for (int i = b0[h]; i < b1[h]; ++i) {
           run += (double)buf[i];
           dst[i] = (float)run;
+          if (coarse && i == end) {
+            coarse[l] = (float)run;
+            end = bins_coarse_end(++l, N);
+          }
         }
       }
     }

@@ -166,9 +166,10 @@ def test_ancestor_bins_equal_indices(stopping, N):
 
 @pytest.mark.parametrize("N", [4096, 1000, 7, 64, 65, 16384])
 def test_bins_index_vs_oracle(N):
-    """smcdet_bins_index (the sweep's 64-ary ancestor search) against the
-    oracle's bucketize of the same weights and offsets: random, degenerate
-    (one particle, a block of zero weights) and uniform weights."""
+    """smcdet_bins_index (the sweep's 64-ary ancestor search, its first level
+    from the chunk-end array) against the oracle's bucketize of the same
+    weights and offsets: random, degenerate (one particle, a block of zero
+    weights) and uniform weights."""
     from oracle import smc_oracle as O
     from smcdet_amd import _hip
     rng = np.random.default_rng(N)
@@ -179,7 +180,11 @@ def test_bins_index_vs_oracle(N):
     U = rng.random(T).astype(np.float32)
     U[-1] = 0.0  # an offset of exactly 0
     bins = np.cumsum(W.astype(np.float64), axis=1).astype(np.float32)  # the tile pass's bins
-    buf = torch.tensor(np.concatenate([bins.ravel(), U]), device=DEV)
+    # the first search level's chunk ends (ABI 17): entry l = bins[min((l+1)c, N) - 1]
+    c = -(-N // 64)
+    ends = np.minimum((np.arange(64) + 1) * c, N) - 1
+    coarse = bins[:, ends]
+    buf = torch.tensor(np.concatenate([bins.ravel(), U, coarse.ravel()]), device=DEV)
     idx = torch.empty(T, N, device=DEV, dtype=torch.int64)
     _hip.check(_hip.lib().smcdet_bins_index(_hip.ptr(buf), T, N, _hip.ptr(idx),
                                             _hip.stream_of(idx)), "bins_index")
