@@ -294,6 +294,65 @@ __device__ __forceinline__ float position_delta_pc(const DevModel& m, const floa
   return pix_delta<MODEL>(m, xs[p], lgx, lo, dl);
 }
 
+// Persisted rate image in / out for tiles of <= 64*PPL pixels: each lane's
+// (at most ceil(PPL/4)) float4 pieces all issued before any is used.
+template <int PPL>
+__device__ __forceinline__ void copy_in_regs(const float* __restrict__ rin, float* lam, int HW,
+                                             int lane) {
+  constexpr int NV = (PPL + 3) / 4;
+  if ((HW & 3) == 0) {
+    float4 v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int p = 4 * (k * kWave + lane);
+      if (p < HW) v[k] = *reinterpret_cast<const float4*>(rin + p);
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int p = 4 * (k * kWave + lane);
+      if (p < HW) {
+        lam[p] = v[k].x;
+        lam[p + 1] = v[k].y;
+        lam[p + 2] = v[k].z;
+        lam[p + 3] = v[k].w;
+      }
+    }
+  } else {
+    float v[PPL];
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+      const int p = k * kWave + lane;
+      if (p < HW) v[k] = rin[p];
+    }
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+      const int p = k * kWave + lane;
+      if (p < HW) lam[p] = v[k];
+    }
+  }
+  wave_sync();
+}
+template <int PPL>
+__device__ __forceinline__ void copy_out_regs(const float* lam, float* __restrict__ rout, int HW,
+                                              int lane) {
+  constexpr int NV = (PPL + 3) / 4;
+  if ((HW & 3) == 0) {
+    float4 v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int p = 4 * (k * kWave + lane);
+      if (p < HW) v[k] = make_float4(lam[p], lam[p + 1], lam[p + 2], lam[p + 3]);
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int p = 4 * (k * kWave + lane);
+      if (p < HW) *reinterpret_cast<float4*>(rout + p) = v[k];
+    }
+  } else {
+    for (int p = lane; p < HW; p += kWave) rout[p] = lam[p];
+  }
+}
+
 // PPL > 0: tiles of <= 64*PPL pixels rendered in registers (render_regs);
 // PPL = 0: LDS render (larger tiles)
 // PAIRED: union-window positions two per lane in packed arithmetic (default);
@@ -429,7 +488,12 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     if (a.rate_in) {
       // the ancestor's rate image, persisted by the previous sweep: no render
       const float* rin = a.rate_in + src * (size_t)HW;
-      if ((HW & 3) == 0) {
+      if constexpr (PPL > 0) {
+        // HW <= 64*PPL (register-render tiles): every lane's float4 loads in
+        // flight before the LDS stores (the generic loop below kept at most
+        // two in flight: one HBM round trip per pair on the sweep's start)
+        copy_in_regs<PPL>(rin, lam, HW, lane);
+      } else if ((HW & 3) == 0) {
         for (int p = 4 * lane; p < HW; p += 4 * kWave) {
           const float4 v = *reinterpret_cast<const float4*>(rin + p);
           lam[p] = v.x;
@@ -461,7 +525,23 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   if constexpr (RV) {
     rv = lam + kMhWaves * HWp;
     wave_sync();
-    for (int p = lane; p < HWp; p += kWave) rv[p] = fast_rcp(fmaf(m.eta, lam[p], m.s0sq));
+    if constexpr (PPL > 0) {
+      // (PPL + 1) cells per lane: the LDS reads first, then the reciprocals
+      constexpr int NR = PPL + 1;
+      float v[NR];
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        const int p = k * kWave + lane;
+        v[k] = p < HWp ? lam[p] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        const int p = k * kWave + lane;
+        if (p < HWp) rv[p] = fast_rcp(fmaf(m.eta, v[k], m.s0sq));
+      }
+    } else {
+      for (int p = lane; p < HWp; p += kWave) rv[p] = fast_rcp(fmaf(m.eta, lam[p], m.s0sq));
+    }
     wave_sync();
   }
   // the PSF cache: row s = source s's raw PSF at every pixel, 0 outside its
@@ -944,7 +1024,9 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   if constexpr (!FULL && !GL) {  // (GL: the sweep worked in rate_out's row)
     if (a.rate_out) {
       float* rout = a.rate_out + pid * (size_t)HW;
-      if ((HW & 3) == 0) {
+      if constexpr (PPL > 0) {
+        copy_out_regs<PPL>(lam, rout, HW, lane);
+      } else if ((HW & 3) == 0) {
         for (int p = 4 * lane; p < HW; p += 4 * kWave)
           *reinterpret_cast<float4*>(rout + p) = make_float4(lam[p], lam[p + 1], lam[p + 2],
                                                              lam[p + 3]);
