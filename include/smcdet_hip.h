@@ -237,10 +237,10 @@ int smcdet_prior_sample(const smcdet_prior_t* prior, int32_t T,
  * be null.  temperature[T].  Outputs: acc_rate[T] = acceptance rate of the
  * LAST iteration (kernel.py:130); loglik_out[T,N] (nullable) = the image
  * log-likelihood of the returned state (what SMCsampler.temper recomputes,
- * sampler.py:100-102).  acc_count[2T] is an int32 workspace that must be
- * zero before the first call; every call leaves it zero again (it holds the
- * per-tile accept counters and workgroup tickets only while the kernel runs),
- * so one zeroed buffer serves every call on a stream.
+ * sampler.py:100-102).  acc_count[2T] is an int32 workspace, 8-byte aligned,
+ * that must be zero before the first call; every call leaves it zero again
+ * (it holds the per-tile accept counters and workgroup tickets only while the
+ * kernel runs), so one zeroed buffer serves every call on a stream.
  * rate_in / rate_out [T,N,H*W] (both nullable, ignored with
  * SMCDET_MH_FULL_RECOMPUTE): persisted per-particle rate images
  * lambda = B + sum_j g f_j psf_j.  With rate_in the sweep starts from the

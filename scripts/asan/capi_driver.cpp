@@ -53,7 +53,7 @@ int main() {
   mh.fluxes_stdev = 2.5f;
   float dummy[16] = {0};
   float* d = dummy;
-  int32_t ws[4] = {0};
+  alignas(8) int32_t ws[4] = {0};
 
   EXPECT(smcdet_loglik(nullptr, d, d, d, 1, 1, 1, d, nullptr), SMCDET_EINVAL);
   EXPECT(smcdet_loglik(&m, nullptr, d, d, 1, 1, 1, d, nullptr), SMCDET_EINVAL);
@@ -82,6 +82,10 @@ int main() {
   EXPECT(smcdet_mh_sweep(&m, &p, &mh, d, d, 1, 4, 65, nullptr, d, d, d, nullptr, d, d, nullptr,
                          nullptr, 0, 0, nullptr, 0, nullptr, d, ws, nullptr, nullptr, nullptr),
          SMCDET_EUNSUPPORTED);
+  // the accept counter is one uint64 per tile: a misaligned workspace is refused
+  EXPECT(smcdet_mh_sweep(&m, &p, &mh, d, d, 1, 4, 10, nullptr, d, d, d, nullptr, d, d, nullptr,
+                         nullptr, 0, 0, nullptr, 0, nullptr, d, ws + 1, nullptr, nullptr, nullptr),
+         SMCDET_EINVAL);
   int64_t anc[4] = {0, 0, 0, 0};
   EXPECT(smcdet_mh_sweep(&m, &p, &mh, d, d, 1, 4, 10, anc, d, d, d, nullptr, d, d, nullptr,
                          nullptr, 0, 0, nullptr, 0, nullptr, d, ws, nullptr, nullptr, nullptr),

@@ -24,6 +24,14 @@ MH_PHASES = ["stage image", "state + tn caches", "initial render", "MH loop", "w
 TILE_PHASES = ["load ll + max", "f(top)", "brentq", "weights", "cumsum", "bins store (or index search)"]
 
 
+def read_raw(name):
+    buf = (ctypes.c_ulonglong * (256 * 16))()
+    fn = getattr(_hip.lib(), name)
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    assert fn(ctypes.addressof(buf), 256 * 16) == 0
+    return np.frombuffer(buf, dtype=np.uint64).reshape(256, 16).astype(np.float64)
+
+
 def read(name, cols):
     buf = (ctypes.c_ulonglong * (256 * 16))()
     fn = getattr(_hip.lib(), name)
@@ -53,11 +61,16 @@ def main():
         torch.cuda.synchronize()
         mh_d = read("smcdet_trace_read_mh", 6)
         tile_d = read("smcdet_trace_read_tile", len(TILE_PHASES) + 1)[:1]
+        # the weights phase's sub-steps (columns 7, 8 lie between 3 and 4)
+        tr = read_raw("smcdet_trace_read_tile")[0]
+        weights_sub = {"exp + partial sums": tr[7] - tr[3], "double reduction": tr[8] - tr[7],
+                       "divide + store": tr[4] - tr[8]}
         out[f"step{i}"] = {
             "tau": float(s.temperature.min()),
             "mh_cycles_mean": dict(zip(MH_PHASES, mh_d.mean(0).round(0).tolist())),
             "mh_cycles_max": dict(zip(MH_PHASES, mh_d.max(0).round(0).tolist())),
             "tile_cycles": dict(zip(TILE_PHASES, tile_d[0].round(0).tolist())),
+            "tile_weights_cycles": weights_sub,
         }
     # wave lifetimes of the last MH sweep: start/end (s_memrealtime, 100 MHz),
     # s_memtime ticks, HW_ID (CU/SIMD placement)

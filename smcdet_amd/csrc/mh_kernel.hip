@@ -85,7 +85,7 @@ struct MhArgs {
   float* rate_out;                   // [T,N,H*W] or null
   const int32_t* go;                 // predicate: skip the launch when *go == 0 (or null)
   const float* boxes;                // [T,4] per-tile location boxes (or null: lb_*/ub_*)
-  int32_t* acc_count;                // [2T] zeroed workspace: counts, tickets
+  int32_t* acc_count;                // [2T] zeroed workspace: [T] uint64 (count << 32 | ticket)
   float* acc_rate;                   // [T]
   const int32_t* r_comp;             // replay (or null)
   const float* r_uloc;
@@ -1053,13 +1053,18 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     // the TAIL build's agent-scope fence above precedes both atomics)
     __threadfence_block();
     if (atomicAdd(&wg_done, 1) == nw - 1) {
-      int32_t* cnt = a.acc_count + t;
-      int32_t* ticket = a.acc_count + a.T + t;
-      atomicAdd(cnt, atomicAdd(&wg_acc, 0));
-      __threadfence();
-      if (atomicAdd(ticket, 1) == (int)gridDim.x - 1) {
-        const int total = atomicExch(cnt, 0);
-        atomicExch(ticket, 0);
+      // the tile's count (high word) and ticket (low word) in ONE 64-bit
+      // atomic: the tile's last workgroup reads every other workgroup's count
+      // in the value it replaces, with no fence between a count and a ticket
+      // (an agent-scope fence is an L2 write-back, right after this
+      // workgroup's rate-image stores).  acc_count [2T] int32 = [T] uint64,
+      // 8-byte aligned (host-checked).
+      unsigned long long* slot = reinterpret_cast<unsigned long long*>(a.acc_count) + t;
+      const unsigned long long mine = (unsigned long long)(unsigned)atomicAdd(&wg_acc, 0);
+      const unsigned long long old = atomicAdd(slot, (mine << 32) | 1ull);
+      if ((unsigned)(old & 0xffffffffull) == gridDim.x - 1) {
+        const unsigned long long total = (old >> 32) + mine;
+        atomicExch(slot, 0ull);
         a.acc_rate[t] = (float)total / (float)N;
         wg_last = 1;
       }
@@ -1385,6 +1390,8 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
   if (!tiled_image || !temperature || !counts_in || !locs_in || !fluxes_in || !locs_out ||
       !fluxes_out || !acc_rate || !acc_count)
     return set_error(SMCDET_EINVAL, "null buffer");
+  if ((uintptr_t)acc_count & 7)
+    return set_error(SMCDET_EINVAL, "acc_count must be 8-byte aligned (one uint64 per tile)");
   if (T <= 0 || N <= 0 || T > 65535) return set_error(SMCDET_EUNSUPPORTED, "T=%d N=%d", T, N);
   if (S < 1 || S > 64) return set_error(SMCDET_EUNSUPPORTED, "S=%d outside 1..64", S);
   if (mh->num_iters < 0) return set_error(SMCDET_EINVAL, "num_iters < 0");

@@ -114,21 +114,27 @@ __device__ __forceinline__ int bins_coarse_end(int l, int N) {
 // tile reached temperature 1, and (last tile, by ticket) the number of tiles
 // still below 1 -- the reference's while condition (sampler.py:230) without
 // extra launches; the counter and ticket are zero again afterwards
+// The count reaches its readers across a launch boundary (the next sweep's
+// `go`; the host after this launch's completion event), which orders it: no
+// system-scope fence here.  A single tile needs no counter either -- and no
+// agent-scope fence, whose L2 write-back sat on the tile pass's path right
+// after the sweep had filled the L2 with rate images.
 __device__ __forceinline__ void tile_status(const TileArgs& a, int t, float tnew) {
   if (a.fin_iter && tnew >= 1.0f && a.fin_iter[t] < 0) a.fin_iter[t] = a.iter;
-  if (a.live) {
+  if (!a.live) return;
+  int nlive;
+  if (a.T == 1) {
+    nlive = tnew < 1.0f ? 1 : 0;
+  } else {
     atomicAdd(&a.live[0], tnew < 1.0f ? 1 : 0);
-    __threadfence();
-    if (atomicAdd(&a.live[1], 1) == a.T - 1) {
-      const int nlive = atomicExch(&a.live[0], 0);
-      a.live[2] = nlive;
-      atomicExch(&a.live[1], 0);
-      if (a.live_host) {  // the host reads it after the launch completes: no copy launch
-        *reinterpret_cast<volatile int32_t*>(a.live_host) = nlive;
-        __threadfence_system();
-      }
-    }
+    __threadfence();  // this tile's count before its ticket
+    if (atomicAdd(&a.live[1], 1) != a.T - 1) return;
+    nlive = atomicExch(&a.live[0], 0);
+    atomicExch(&a.live[1], 0);
   }
+  a.live[2] = nlive;
+  // the host reads it after the launch completes: no copy launch
+  if (a.live_host) *reinterpret_cast<volatile int32_t*>(a.live_host) = nlive;
 }
 
 // Per-virtual-wave partials of the workgroup reductions, double-buffered.
@@ -556,8 +562,10 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
     }
     // one reduction for the sum and the sum of squares: ESS = 1 / sum W^2
     // = (sum e)^2 / sum e^2 (sampler.py:187-190), in double
+    SMC_TRACE(trow, 7);
     double se, qe;
     vblock_sum2d<NT>(ssum, qsum, se, qe, &red, parity);
+    SMC_TRACE(trow, 8);
     const float sf = (float)se;
 #pragma unroll
     for (int h = 0; h < VPT; ++h) {
