@@ -349,7 +349,7 @@ int smcdet_resample_index(const float* weights, int32_t T, int32_t N,
  * launch per SMC iteration instead of three.  flags: SMCDET_SMC_*.
  * finished_iter [T] (nullable, int32): set to `iter` when a tile's
  * temperature reaches 1 while it holds a negative value (per-tile finishing
- * iteration).  live [3] (nullable, int32, zero before the first call): after
+ * iteration).  live [3] (nullable, int32, 8-byte aligned, zero before the first call): after
  * the call live[2] = the number of tiles still below temperature 1 (the
  * reference's while condition, sampler.py:230); live[0..1] are workspace and
  * left zero.  go (nullable): when *go == 0 the launch does nothing.

@@ -1499,6 +1499,8 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
     ta.smc_flags = tail->flags & ~SMCDET_SMC_TWO_LAUNCH;
     ta.fin_iter = tail->finished_iter;
     ta.iter = tail->iter;
+    if ((uintptr_t)tail->live & 7)
+      return set_error(SMCDET_EINVAL, "tail->live must be 8-byte aligned");
     ta.live = tail->live;
     ta.live_host = tail->live ? tail->live_host : nullptr;
     size_t lds_f = 0;

@@ -467,6 +467,7 @@ int smcdet_temper_reweight(const float* loglik, float* temperature, float* tempe
   a.smc_flags = flags;
   a.fin_iter = finished_iter;
   a.iter = iter;
+  if ((uintptr_t)live & 7) return set_error(SMCDET_EINVAL, "live must be 8-byte aligned");
   a.live = live;
   a.go = go;
   a.live_host = live ? live_host : nullptr;

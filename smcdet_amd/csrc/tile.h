@@ -58,7 +58,7 @@ struct TileArgs {
   uint32_t smc_flags;        // SMCDET_SMC_*
   int32_t* fin_iter;         // [T] SMC iteration a tile reached temperature 1 (-1: not yet) or null
   int32_t iter;              // the caller's SMC iteration number
-  int32_t* live;             // [3] zeroed workspace: counter, ticket, tiles still below 1 (or null)
+  int32_t* live;             // [3] zeroed workspace, 8-byte aligned: counter, ticket, tiles still below 1 (or null)
   const int32_t* go;         // predicate: skip the launch when *go == 0 (or null)
   int32_t* live_host;        // host-mapped copy of live[2] (pinned host memory) or null
   float* bins_out;           // [T*N + T] systematic bins + offsets instead of idx (or null)
@@ -116,21 +116,23 @@ __device__ __forceinline__ int bins_coarse_end(int l, int N) {
 // extra launches; the counter and ticket are zero again afterwards
 // The count reaches its readers across a launch boundary (the next sweep's
 // `go`; the host after this launch's completion event), which orders it: no
-// system-scope fence here.  A single tile needs no counter either -- and no
-// agent-scope fence, whose L2 write-back sat on the tile pass's path right
-// after the sweep had filled the L2 with rate images.
+// system-scope fence here, and no agent-scope one between the tiles' counts
+// and tickets either (one 64-bit atomic carries both): such a fence is an L2
+// write-back, on the tile pass's path right after the sweep filled the L2
+// with rate images.
 __device__ __forceinline__ void tile_status(const TileArgs& a, int t, float tnew) {
   if (a.fin_iter && tnew >= 1.0f && a.fin_iter[t] < 0) a.fin_iter[t] = a.iter;
   if (!a.live) return;
-  int nlive;
-  if (a.T == 1) {
-    nlive = tnew < 1.0f ? 1 : 0;
-  } else {
-    atomicAdd(&a.live[0], tnew < 1.0f ? 1 : 0);
-    __threadfence();  // this tile's count before its ticket
-    if (atomicAdd(&a.live[1], 1) != a.T - 1) return;
-    nlive = atomicExch(&a.live[0], 0);
-    atomicExch(&a.live[1], 0);
+  int nlive = tnew < 1.0f ? 1 : 0;
+  if (a.T > 1) {
+    // count (high word) and ticket (low word) of live[0..1] in one 64-bit
+    // atomic: the last tile reads every other tile's count in the value it
+    // replaces, no fence between a count and a ticket (live: 8-byte aligned)
+    unsigned long long* slot = reinterpret_cast<unsigned long long*>(a.live);
+    const unsigned long long old = atomicAdd(slot, ((unsigned long long)nlive << 32) | 1ull);
+    if ((int)(old & 0xffffffffull) != a.T - 1) return;
+    nlive += (int)(old >> 32);
+    atomicExch(slot, 0ull);
   }
   a.live[2] = nlive;
   // the host reads it after the launch completes: no copy launch
