@@ -54,7 +54,7 @@ def main():
     pr.disable()
     torch.cuda.synchronize()
     out = io.StringIO()
-    pstats.Stats(pr, stream=out).sort_stats("tottime").print_stats(25)
+    pstats.Stats(pr, stream=out).sort_stats("tottime").print_stats(40)
     print(out.getvalue())
 
 
