@@ -58,10 +58,10 @@ struct TileArgs {
   uint32_t smc_flags;        // SMCDET_SMC_*
   int32_t* fin_iter;         // [T] SMC iteration a tile reached temperature 1 (-1: not yet) or null
   int32_t iter;              // the caller's SMC iteration number
-  int32_t* live;             // [3] zeroed workspace, 8-byte aligned: counter, ticket, tiles still below 1 (or null)
+  int32_t* live;             // [3] zeroed, 8-byte aligned: count, ticket, tiles below 1 (or null)
   const int32_t* go;         // predicate: skip the launch when *go == 0 (or null)
   int32_t* live_host;        // host-mapped copy of live[2] (pinned host memory) or null
-  float* bins_out;           // [T*N + T] systematic bins + offsets instead of idx (or null)
+  float* bins_out;           // [T*N + 65T] bins, offsets U, chunk ends, instead of idx (or null)
 };
 
 // one tile pass launch (smc_kernels.hip)
@@ -93,7 +93,9 @@ __device__ __forceinline__ int bins_ancestor(const float* __restrict__ bins,
     // below the key means the whole chunk is (bins are monotone)
     const int step = (len + 63) >> 6;
     const bool valid = lane * step < len;
-    const float b = !valid ? 0.f : first ? coarse[lane] : bins[lo + min((lane + 1) * step, len) - 1];
+    const float b = !valid ? 0.f
+                  : first ? coarse[lane]
+                          : bins[lo + min((lane + 1) * step, len) - 1];
     first = false;
     const bool less = valid && (pow2 ? (b * Nf < key) : (b < key));
     const int c = __popcll(__ballot(less));
