@@ -4,7 +4,7 @@
 # pmc_mh_r04.json), and a PMC pass of the opt-in PSF-table sweep (LDS
 # instructions and bank conflicts, the A/B's cause).  Each GPU step has its
 # own limit; a crash, abort or timeout ends the script (test failures, rc 1,
-# do not).  STEPS selects: tests bench profile tbpmc newtests
+# do not).  STEPS selects: tests bench profile tbpmc postbench
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -42,4 +42,12 @@ if has tbpmc; then
     SUMMARY=$D/pmc_mh_tb.json bash scripts/profile.sh
   step tbpmc $?
   tail -12 $D/prof_tb/summary.txt
+fi
+if has postbench; then
+  # the bench line with this pass's counters: the PMC summary (same library
+  # source hash) goes where bench.py reads it, then the default bench runs
+  cp $D/pmc_mh_r04.json profiles/pmc_mh_r04.json
+  timeout -k 10 400 python bench.py > $D/bench_post.log 2>&1
+  step postbench $?
+  tail -c 400 $D/bench_post.log; echo
 fi
