@@ -137,3 +137,22 @@ def test_struct_caches_follow_rebinding():
     assert prior._cprior() is p1
     prior.max_objects = 9
     assert prior._cprior().max_objects == 9
+
+
+def test_ancestor_bins_buffer_layout():
+    """AncestorBins (ABI 17): per tile N running sums, then the T offsets, then
+    per tile the 64 chunk ends of the search's first level -- the
+    SMCDET_BINS_FLOATS(T, N) = T*N + 65*T floats the header names; as_index
+    passes int64 index tensors through."""
+    import re
+
+    from smcdet_amd import _hip
+    b = _hip.AncestorBins.empty((2, 3, 100), torch.device("cpu"))
+    assert b.shape == (2, 3, 100) and b.buf.dtype == torch.float32
+    assert b.buf.numel() == 6 * 100 + 65 * 6
+    hdr = open(_hip.SOURCES[-1]).read()
+    m = re.search(r"#define SMCDET_BINS_FLOATS\(T, N\) \(\(size_t\)\(T\) \* \(size_t\)\(N\) \+ "
+                  r"\(size_t\)\(T\) \* (\d+)u\)", hdr)
+    assert m and int(m.group(1)) == 65
+    idx = torch.zeros(1, 1, 4, dtype=torch.int64)
+    assert _hip.as_index(idx) is idx and _hip.as_index(None) is None
