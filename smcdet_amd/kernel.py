@@ -124,7 +124,9 @@ class SingleComponentMH(object):
             image_model=None, ancestors=None, replay=None, want_loglik=True, rate_in=None,
             rate_out=None, flags=0, go=None, tile_boxes=None, tail=None, tail_take=0):
         """kernel.py:26-130.  ancestors [numH,numW,N] (int64, optional) gathers
-        the starting state (a fused resample); replay = dict(comp, uloc, uflux,
+        the starting state (a fused resample); with the fused step's `tail`
+        it may instead be an _hip.AncestorBins (the previous tile pass's bins:
+        each wave of the sweep finds its own ancestor); replay = dict(comp, uloc, uflux,
         uacc) replays recorded draws; rate_in / rate_out [numH,numW,N,H*W]
         (optional) are persisted per-particle rate images: rate_in must be the
         images of (locs, fluxes), rate_out receives those of the result
