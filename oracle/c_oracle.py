@@ -12,6 +12,7 @@ from . import smc_oracle as O
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libmh_oracle.so")
+LIB_F32 = os.path.join(HERE, "libmh_oracle_f32.so")
 
 
 class _Model(ctypes.Structure):
@@ -32,6 +33,7 @@ class _MH(ctypes.Structure):
 
 
 _lib = None
+_lib_f32 = None
 
 
 def build():
@@ -47,7 +49,28 @@ def lib():
         _lib.mh_oracle_sweep.restype = ctypes.c_int
         _lib.mala_oracle_sweep.restype = ctypes.c_int
         _lib.mh_oracle_loglik.restype = ctypes.c_int
+        _lib.mh_oracle_sweep_cached.restype = ctypes.c_int
+        _lib.mh_oracle_loglik_cached.restype = ctypes.c_int
     return _lib
+
+
+def lib_f32():
+    """The float32 arithmetic-class build (mh_oracle.c -DOM_F32): only the
+    cached sweep and the log-likelihood."""
+    global _lib_f32
+    if _lib_f32 is None:
+        if not os.path.exists(LIB_F32):
+            build()
+        _lib_f32 = ctypes.CDLL(LIB_F32)
+        _lib_f32.mh_oracle_sweep_cached.restype = ctypes.c_int
+        _lib_f32.mh_oracle_loglik_cached.restype = ctypes.c_int
+    return _lib_f32
+
+
+def _arith_lib(arith):
+    if arith not in ("f64", "f32"):
+        raise ValueError(f"arith must be 'f64' or 'f32', not {arith!r}")
+    return lib_f32() if arith == "f32" else lib()
 
 
 def _pack(model, prior, mh):
@@ -81,9 +104,13 @@ def _pack(model, prior, mh):
 
 
 def mh_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mh, replay=None, seed=0,
-             threads=0, frozen_out=False):
+             threads=0, frozen_out=False, cached=False, arith="f64"):
     """Runs the C sweep; returns (locs, fluxes, acc_rate[nH,nW]) (+ the
-    [nH,nW,N] mask of particles frozen by an upper-edge proposal)."""
+    [nH,nW,N] mask of particles frozen by an upper-edge proposal).
+    cached=True: the cached re-render (mh_oracle_sweep_cached; bit-identical
+    in float64); arith="f32": its float32 arithmetic-class build."""
+    if arith != "f64" and not cached:
+        raise ValueError("the float32 build has the cached sweep only")
     img = np.ascontiguousarray(tiled_image, dtype=np.float32)
     nH, nW, N, S, _ = np.shape(locs)
     T = nH * nW
@@ -100,9 +127,16 @@ def mh_sweep(tiled_image, counts, locs, fluxes, tau, prior, model, mh, replay=No
         ru = np.ascontiguousarray(replay["uloc"], dtype=np.float32)
         rf = np.ascontiguousarray(replay["uflux"], dtype=np.float32)
         ra = np.ascontiguousarray(replay["uacc"], dtype=np.float32)
-    lib().mh_oracle_sweep(ctypes.byref(m), ctypes.byref(p), ctypes.byref(h), P(img), P(c), P(l),
-                          P(f), P(t), T, N, S, P(rc_), P(ru), P(rf), P(ra),
-                          ctypes.c_uint64(seed), threads, P(acc))
+    if cached:
+        upper = float(getattr(prior, "flux_upper", 0.0))
+        _arith_lib(arith).mh_oracle_sweep_cached(
+            ctypes.byref(m), ctypes.byref(p), ctypes.byref(h), P(img), P(c), P(l), P(f), P(t), T,
+            N, S, P(rc_), P(ru), P(rf), P(ra), ctypes.c_uint64(seed), threads, P(acc),
+            ctypes.c_double(upper))
+    else:
+        lib().mh_oracle_sweep(ctypes.byref(m), ctypes.byref(p), ctypes.byref(h), P(img), P(c),
+                              P(l), P(f), P(t), T, N, S, P(rc_), P(ru), P(rf), P(ra),
+                              ctypes.c_uint64(seed), threads, P(acc))
     acc = acc.reshape(nH, nW, N)
     rate = (acc == 1).mean(-1)
     return (l, f, rate, acc == 2) if frozen_out else (l, f, rate)
@@ -135,9 +169,10 @@ def sweep_draws(seed, T, N, K, S):
             "uacc": out[:, 4].astype(np.float32).reshape(K, T, N)}
 
 
-def loglik(tiled_image, locs, fluxes, model, threads=0):
-    """Image log-likelihoods [nH,nW,N] (float64) of the catalogs, by the C
-    restatement (images.py:159-175 / :85-102)."""
+def loglik(tiled_image, locs, fluxes, model, threads=0, arith="f64"):
+    """Image log-likelihoods [nH,nW,N] (float64 array) of the catalogs, by the
+    C restatement (images.py:159-175 / :85-102); arith="f32": computed in the
+    float32 build (values are float32 numbers)."""
     img = np.ascontiguousarray(tiled_image, dtype=np.float32)
     nH, nW, N, S, _ = np.shape(locs)
     l = np.ascontiguousarray(locs, dtype=np.float32)
@@ -147,7 +182,8 @@ def loglik(tiled_image, locs, fluxes, model, threads=0):
         if isinstance(model, O.M71Model) else O.ParetoPriorP(S, S, model.H, model.W, 0, 1.0, 1.0)
     m, _, _ = _pack(model, prior, O.MHParams(0, 1.0, 1.0, 0.1, 1.0))
     P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
-    lib().mh_oracle_loglik(ctypes.byref(m), P(img), P(l), P(f), nH * nW, N, S, threads, P(out))
+    fn = lib().mh_oracle_loglik if arith == "f64" else _arith_lib(arith).mh_oracle_loglik_cached
+    fn(ctypes.byref(m), P(img), P(l), P(f), nH * nW, N, S, threads, P(out))
     return out.reshape(nH, nW, N)
 
 

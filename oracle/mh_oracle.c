@@ -192,6 +192,7 @@ static double urand(uint64_t* s) { return (double)(splitmix(s) >> 40) * (1.0 / 1
  * accumulation as loglik() above: out[T*N].  For the oracle SMC runs
  * (tests/golden/make_oracle_stats.py).  Returns 0.
  */
+#ifndef OM_F32 /* float64 build only */
 int mh_oracle_loglik(const om_model_t* m, const float* image, const float* locs,
                      const float* fluxes, int T, int N, int S, int threads, double* out) {
   const int HW = m->H * m->W;
@@ -221,6 +222,8 @@ int mh_oracle_loglik(const om_model_t* m, const float* image, const float* locs,
   }
   return 0;
 }
+#endif
+
 
 /*
  * One MH sweep over T*N particles.  image [T,H,W], counts [T,N], locs
@@ -230,6 +233,7 @@ int mh_oracle_loglik(const om_model_t* m, const float* image, const float* locs,
  * receives the accept flag of the last iteration (2: the particle was frozen
  * by an upper-edge proposal, a rejection).  Returns 0.
  */
+#ifndef OM_F32 /* float64 build only */
 int mh_oracle_sweep(const om_model_t* m, const om_prior_t* pr, const om_mh_t* mh,
                     const float* image, const float* counts, float* locs, float* fluxes,
                     const float* tau, int T, int N, int S, const int32_t* comp,
@@ -327,6 +331,8 @@ int mh_oracle_sweep(const om_model_t* m, const om_prior_t* pr, const om_mh_t* mh
   }
   return 0;
 }
+#endif
+
 
 /* ------------------------------------------------------------------------
  * SingleComponentMALA.run (smcdet/kernel.py:133-275).
@@ -438,6 +444,7 @@ static double log_prior_var(const om_prior_t* pr, const double* h, const double*
  * gradient at the current state w.r.t. the chosen source's (h, w, f) each
  * iteration, prop_out (nullable) [K,T,N,3] the proposal.
  */
+#ifndef OM_F32 /* float64 build only */
 int mala_oracle_sweep(const om_model_t* m, const om_prior_t* pr, const om_mh_t* mh,
                       const float* image, const float* counts, float* locs, float* fluxes,
                       const float* tau, int T, int N, int S, const int32_t* comp,
@@ -555,6 +562,423 @@ int mala_oracle_sweep(const om_model_t* m, const om_prior_t* pr, const om_mh_t* 
     }
     free(h);
     free(rate < rate_p ? rate : rate_p);
+  }
+  return 0;
+}
+#endif
+
+
+/* ------------------------------------------------------------------------
+ * The MH sweep again, with cached per-source PSF windows, in `real`
+ * arithmetic (the oracle's statistics runs, tests/golden/make_oracle_stats.py).
+ *
+ * A proposal moves one source, so only its new window is evaluated; the rate
+ * of every pixel in the bounding box of the old and new windows is re-summed
+ * from the cached contributions in source order, and the log-likelihood is
+ * re-summed over all pixels in pixel order from cached per-pixel terms.
+ * Every value is therefore the one the full re-render of mh_oracle_sweep
+ * computes, with the same operations in the same order: in the float64 build
+ * the two sweeps are bit-identical (tests/test_oracle_cached.py), at ~1/4 of
+ * the cost.
+ *
+ * Built twice (oracle/Makefile):
+ *   libmh_oracle.so      real = double, the float64 oracle above;
+ *   libmh_oracle_f32.so  real = float (-DOM_F32): the reference's float32
+ *     arithmetic class -- PSF from r = |p + 0.5 - loc| and r**2
+ *     (images.py:45, :137-145), rate = sum_s psf * (adu * f) + B
+ *     (:162-167), torch's Normal.log_prob form (var = scale**2, log scale)
+ *     summed in float32 (:169-175), float32 proposals and Hastings terms
+ *     (distributions.py:40-52) and log target = log prior + tau * loglik with
+ *     log numerator / denominator composed as kernel.py:64-116 does.
+ * ---------------------------------------------------------------------- */
+#ifdef OM_F32
+typedef float real;
+#define R_EXP expf
+#define R_LOG logf
+#define R_POW powf
+#define R_SQRT sqrtf
+#define R_FLOOR floorf
+#else
+typedef double real;
+#define R_EXP exp
+#define R_LOG log
+#define R_POW pow
+#define R_SQRT sqrt
+#define R_FLOOR floor
+#endif
+
+typedef struct {
+  int fh, fw;         /* window anchor floor(loc) */
+  int r0, r1, c0, c1; /* window clipped to the tile (r0 > r1: empty) */
+} om_win_t;
+
+static void win_of(const om_model_t* m, real h, real w, om_win_t* d) {
+  const int R = m->R;
+  d->fh = (int)R_FLOOR(h);
+  d->fw = (int)R_FLOOR(w);
+  d->r0 = d->fh - R < 0 ? 0 : d->fh - R;
+  d->r1 = d->fh + R > m->H - 1 ? m->H - 1 : d->fh + R;
+  d->c0 = d->fw - R < 0 ? 0 : d->fw - R;
+  d->c1 = d->fw + R > m->W - 1 ? m->W - 1 : d->fw + R;
+}
+
+static inline int win_has(const om_win_t* d, int ph, int pw) {
+  return ph >= d->r0 && ph <= d->r1 && pw >= d->c0 && pw <= d->c1;
+}
+
+/* psf(pixel) * (adu * f) of one source over its clipped window, into
+ * c[(ph - fh + R) * (2R + 1) + (pw - fw + R)] */
+static void contrib(const om_model_t* m, real h, real w, real f, const om_win_t* d, real* c) {
+  const int R = m->R, D = 2 * R + 1;
+#ifdef OM_F32
+  const real gf = (real)m->g * f;
+#endif
+  for (int ph = d->r0; ph <= d->r1; ++ph)
+    for (int pw = d->c0; pw <= d->c1; ++pw) {
+      real v;
+#ifdef OM_F32
+      /* images.py:31-45: pixel = floor(loc) + offset; r = |pixel + 0.5 - loc| */
+      const real dh = ((real)ph + 0.5f) - h, dw = ((real)pw + 0.5f) - w;
+      const real r = R_SQRT(dh * dh + dw * dw), r2 = r * r;
+      if (m->model == 1) {
+        const real t1 = R_EXP(-r2 / (real)(2 * m->s1));
+        const real t2 = (real)m->b * R_EXP(-r2 / (real)(2 * m->s2));
+        const real t3 = (real)m->p0 * R_POW(1 + r2 / (real)(m->beta * m->sp), (real)(-m->beta / 2));
+        v = ((t1 + t2) + t3) / (real)(1 + m->b + m->p0) / (real)m->norm;
+      } else {
+        const real s = (real)m->psf_stdev;
+        v = R_EXP(-r2 / (2 * s * s) - R_LOG(s) - (real)(0.5 * log(2 * M_PI)));
+      }
+      v = v * gf;
+#else
+      const double dh = ph + 0.5 - h, dw = pw + 0.5 - w;
+      v = psf_value(m, dh * dh + dw * dw) * (m->g * f);
+#endif
+      c[(ph - d->fh + R) * D + (pw - d->fw + R)] = v;
+    }
+}
+
+/* one pixel's log-likelihood term at rate (without background) `rate` */
+static inline real pix_term(const om_model_t* m, real xp, real rate, real lgx) {
+  const real lam = rate + (real)m->bg;
+#ifdef OM_F32
+  if (m->model == 1) {
+    /* Normal(lam, sqrt(s0 + eta lam)).log_prob(x): torch's operation order */
+    const real scale = R_SQRT((real)m->s0sq + (real)m->eta * lam);
+    const real var = scale * scale;
+    const real d = xp - lam;
+    return -(d * d) / (2 * var) - R_LOG(scale) - (real)0.91893853320467274178;
+  } else if (lam > 50000.0f) {
+    const real scale = R_SQRT(lam), var = scale * scale, d = xp - lam;
+    return -(d * d) / (2 * var) - R_LOG(scale) - (real)0.91893853320467274178;
+  }
+  return (xp == 0 ? 0.0f : xp * R_LOG(lam)) - lam - lgx;
+#else
+  if (m->model == 1) {
+    const double v = m->s0sq + m->eta * lam;
+    return -(xp - lam) * (xp - lam) / (2 * v) - 0.5 * log(v) - 0.5 * log(2 * M_PI);
+  } else if (lam > 50000.0) {
+    return -(xp - lam) * (xp - lam) / (2 * lam) - 0.5 * log(lam) - 0.5 * log(2 * M_PI);
+  }
+  return (xp == 0 ? 0.0 : xp * log(lam)) - lam - lgx;
+#endif
+}
+
+typedef struct {
+  int S, HW, D2;
+  real *h, *w, *f;
+  om_win_t* win;
+  real* cv;   /* [S][D2] cached contributions */
+  real* cnew; /* [D2] */
+  real* term; /* [HW] */
+  real* tb;   /* [HW] bounding-box terms */
+  real* lgx;  /* [HW] */
+} om_ws_t;
+
+static void ws_alloc(om_ws_t* s, const om_model_t* m, int S) {
+  const int D = 2 * m->R + 1;
+  s->S = S;
+  s->HW = m->H * m->W;
+  s->D2 = D * D;
+  s->h = malloc(sizeof(real) * 3 * S);
+  s->w = s->h + S;
+  s->f = s->w + S;
+  s->win = malloc(sizeof(om_win_t) * S);
+  s->cv = malloc(sizeof(real) * ((size_t)S + 1) * s->D2);
+  s->cnew = s->cv + (size_t)S * s->D2;
+  s->term = malloc(sizeof(real) * 3 * s->HW);
+  s->tb = s->term + s->HW;
+  s->lgx = s->tb + s->HW;
+}
+
+static void ws_free(om_ws_t* s) {
+  free(s->h);
+  free(s->win);
+  free(s->cv);
+  free(s->term);
+}
+
+/* rate (without background) at pixel (ph, pw): the cached contributions of
+ * the sources whose window holds it, summed in source order; source j's
+ * from cj / wj instead of the cache when cj != NULL */
+static inline real rate_at(const om_model_t* m, const om_ws_t* s, int ph, int pw, int j,
+                           const real* cj, const om_win_t* wj) {
+  const int R = m->R, D = 2 * R + 1;
+  real r = 0;
+  for (int k = 0; k < s->S; ++k) {
+    const om_win_t* d = (k == j && cj) ? wj : &s->win[k];
+    if (!win_has(d, ph, pw)) continue;
+    const real* c = (k == j && cj) ? cj : s->cv + (size_t)k * s->D2;
+    r += c[(ph - d->fh + R) * D + (pw - d->fw + R)];
+  }
+  return r;
+}
+
+/* render every source into the cache and the per-pixel terms; returns the
+ * log-likelihood (the sum of the terms in pixel order, as loglik()) */
+static real ws_render(const om_model_t* m, om_ws_t* s, const float* x) {
+  for (int k = 0; k < s->S; ++k) {
+    win_of(m, s->h[k], s->w[k], &s->win[k]);
+    contrib(m, s->h[k], s->w[k], s->f[k], &s->win[k], s->cv + (size_t)k * s->D2);
+  }
+  real ll = 0;
+  for (int ph = 0; ph < m->H; ++ph)
+    for (int pw = 0; pw < m->W; ++pw) {
+      const int p = ph * m->W + pw;
+      s->term[p] = pix_term(m, x[p], rate_at(m, s, ph, pw, -1, NULL, NULL), s->lgx[p]);
+      ll += s->term[p];
+    }
+  return ll;
+}
+
+/* log-likelihood with source j moved to (h, w, f) (the caller has set
+ * s->h/w/f[j]); its window and contributions into *wj / s->cnew, the terms
+ * of the bounding box [b0..b1] x [b2..b3] of its old and new windows into
+ * s->tb (row-major over the box) */
+static real ws_propose(const om_model_t* m, om_ws_t* s, const float* x, int j, om_win_t* wj,
+                       int* bb) {
+  win_of(m, s->h[j], s->w[j], wj);
+  contrib(m, s->h[j], s->w[j], s->f[j], wj, s->cnew);
+  const om_win_t* o = &s->win[j];
+  const int oe = o->r0 > o->r1 || o->c0 > o->c1, ne = wj->r0 > wj->r1 || wj->c0 > wj->c1;
+  int b0, b1, b2, b3;
+  if (oe && ne) {
+    b0 = 0, b1 = -1, b2 = 0, b3 = -1;
+  } else if (oe) {
+    b0 = wj->r0, b1 = wj->r1, b2 = wj->c0, b3 = wj->c1;
+  } else if (ne) {
+    b0 = o->r0, b1 = o->r1, b2 = o->c0, b3 = o->c1;
+  } else {
+    b0 = o->r0 < wj->r0 ? o->r0 : wj->r0;
+    b1 = o->r1 > wj->r1 ? o->r1 : wj->r1;
+    b2 = o->c0 < wj->c0 ? o->c0 : wj->c0;
+    b3 = o->c1 > wj->c1 ? o->c1 : wj->c1;
+  }
+  bb[0] = b0, bb[1] = b1, bb[2] = b2, bb[3] = b3;
+  const int bw = b3 - b2 + 1;
+  for (int ph = b0; ph <= b1; ++ph)
+    for (int pw = b2; pw <= b3; ++pw) {
+      const int p = ph * m->W + pw;
+      s->tb[(ph - b0) * bw + (pw - b2)] =
+          pix_term(m, x[p], rate_at(m, s, ph, pw, j, s->cnew, wj), s->lgx[p]);
+    }
+  real ll = 0;
+  for (int ph = 0; ph < m->H; ++ph) {
+    const int inr = ph >= b0 && ph <= b1;
+    for (int pw = 0; pw < m->W; ++pw)
+      ll += (inr && pw >= b2 && pw <= b3) ? s->tb[(ph - b0) * bw + (pw - b2)]
+                                          : s->term[ph * m->W + pw];
+  }
+  return ll;
+}
+
+static void ws_accept(const om_model_t* m, om_ws_t* s, int j, const om_win_t* wj, const int* bb) {
+  s->win[j] = *wj;
+  memcpy(s->cv + (size_t)j * s->D2, s->cnew, sizeof(real) * s->D2);
+  const int bw = bb[3] - bb[2] + 1;
+  for (int ph = bb[0]; ph <= bb[1]; ++ph)
+    for (int pw = bb[2]; pw <= bb[3]; ++pw)
+      s->term[ph * m->W + pw] = s->tb[(ph - bb[0]) * bw + (pw - bb[2])];
+}
+
+#ifdef OM_F32
+/* the state-dependent log prior in float32 (prior.py:67-75 + :220-226 /
+ * :183-189): per active source 2 x log(1 / (high - low)) + the flux term
+ * log_norm - (alpha + 1) log f, masked-summed over sources in order */
+static float log_prior_f(const om_prior_t* pr, const float* f, int S, double cnt, float lu_h,
+                         float lu_w, float lnorm) {
+  float lp = 0.0f;
+  for (int s = 0; s < S; ++s) {
+    const float act = s < cnt ? 1.0f : 0.0f;
+    lp += (lu_h + lu_w) * act;
+  }
+  for (int s = 0; s < S; ++s) {
+    const float act = s < cnt ? 1.0f : 0.0f;
+    const float fv = f[s] == 0 ? (float)pr->lower : f[s];
+    lp += (lnorm - ((float)pr->alpha + 1.0f) * logf(fv)) * act;
+  }
+  return lp;
+}
+#endif
+
+/*
+ * mh_oracle_sweep with the cached re-render; same arguments and results (and
+ * the same seeded stream).  `upper` is the flux prior's upper bound (used by
+ * the float32 build's log-prior constant only).
+ */
+int mh_oracle_sweep_cached(const om_model_t* m, const om_prior_t* pr, const om_mh_t* mh,
+                           const float* image, const float* counts, float* locs, float* fluxes,
+                           const float* tau, int T, int N, int S, const int32_t* comp,
+                           const float* uloc, const float* uflux, const float* uacc,
+                           uint64_t seed, int threads, uint8_t* acc_last, double upper) {
+  const int HW = m->H * m->W;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#endif
+#ifdef OM_F32
+  const float sl = (float)mh->sl, sf = (float)mh->sf;
+  const float rsl = 1.0f / sl, rsf = 1.0f / sf;
+  const float lbh = (float)mh->lb_h, lbw = (float)mh->lb_w, ubh = (float)mh->ub_h;
+  const float ubw = (float)mh->ub_w, lbf = (float)mh->lb_f, ubf = (float)mh->ub_f;
+  const float lu_h = -logf((float)pr->loc_high_h - (float)pr->loc_low);
+  const float lu_w = -logf((float)pr->loc_high_w - (float)pr->loc_low);
+  const float a = (float)pr->alpha, L = (float)pr->lower, U = (float)upper;
+  const float lnorm = logf(a) + a * logf(L) + a * logf(U) - logf(powf(U, a) - powf(L, a));
+#else
+  (void)upper;
+#endif
+#pragma omp parallel
+  {
+    om_ws_t ws;
+    ws_alloc(&ws, m, S);
+#pragma omp for schedule(dynamic, 4)
+    for (long pid = 0; pid < (long)T * N; ++pid) {
+      const int t = (int)(pid / N);
+      const float* x = image + (size_t)t * HW;
+      for (int p = 0; p < HW; ++p) ws.lgx[p] = (real)lgamma((double)x[p] + 1.0);
+      for (int s = 0; s < S; ++s) {
+        ws.h[s] = locs[(pid * S + s) * 2 + 0];
+        ws.w[s] = locs[(pid * S + s) * 2 + 1];
+        ws.f[s] = fluxes[pid * S + s];
+      }
+      const double cnt = counts[pid];
+      uint64_t st = seed ^ (0xA5A5A5A5ull * (uint64_t)(pid + 1));
+      real ll = ws_render(m, &ws, x);
+#ifdef OM_F32
+      float lt = log_prior_f(pr, ws.f, S, cnt, lu_h, lu_w, lnorm) + tau[t] * ll;
+#endif
+      int acc = 0;
+      for (int k = 0; k < mh->K; ++k) {
+        int j;
+        double uh, uw, uf, ua;
+        if (comp) {
+          const size_t r = ((size_t)k * T + t) * N + (pid % N);
+          j = comp[r];
+          uh = uloc[r * 2];
+          uw = uloc[r * 2 + 1];
+          uf = uflux[r];
+          ua = uacc[r];
+        } else {
+          j = (int)(urand(&st) * S);
+          if (j >= S) j = S - 1;
+          uh = urand(&st);
+          uw = urand(&st);
+          uf = urand(&st);
+          ua = urand(&st);
+        }
+        const real oh = ws.h[j], ow = ws.w[j], of = ws.f[j];
+#ifdef OM_F32
+        const float nh = tn_sample_f(oh, sl, rsl, lbh, ubh, (float)uh);
+        const float nw = tn_sample_f(ow, sl, rsl, lbw, ubw, (float)uw);
+        const float nf = tn_sample_f(of, sf, rsf, lbf, ubf, (float)uf);
+#else
+        const double nh = (float)tn_sample(oh, mh->sl, mh->lb_h, mh->ub_h, uh);
+        const double nw = (float)tn_sample(ow, mh->sl, mh->lb_w, mh->ub_w, uw);
+        const double nf = (float)tn_sample(of, mh->sf, mh->lb_f, mh->ub_f, uf);
+#endif
+        if (nh >= pr->loc_high_h || nw >= pr->loc_high_w) {
+          acc = 2; /* upper-edge proposal: rejected and frozen (see mh_oracle_sweep) */
+          break;
+        }
+        ws.h[j] = nh;
+        ws.w[j] = nw;
+        ws.f[j] = nf;
+        om_win_t wj;
+        int bb[4];
+        const real nll = ws_propose(m, &ws, x, j, &wj, bb);
+#ifdef OM_F32
+        /* kernel.py:64-116: TruncatedDiagonalMVN(proposed).log_prob(prev) etc. */
+        const float nq_l = tn_logprob_f(oh, nh, sl, rsl, lbh, ubh) +
+                           tn_logprob_f(ow, nw, sl, rsl, lbw, ubw);
+        const float nq_f = tn_logprob_f(of, nf, sf, rsf, lbf, ubf);
+        const float dq_l = tn_logprob_f(nh, oh, sl, rsl, lbh, ubh) +
+                           tn_logprob_f(nw, ow, sl, rsl, lbw, ubw);
+        const float dq_f = tn_logprob_f(nf, of, sf, rsf, lbf, ubf);
+        const float lt_p = log_prior_f(pr, ws.f, S, cnt, lu_h, lu_w, lnorm) + tau[t] * nll;
+        const float num = (lt_p + nq_l) + nq_f;
+        const float den = (lt + dq_l) + dq_f;
+        float alpha = expf(num - den);
+        if (alpha > 1.0f) alpha = 1.0f;
+        acc = (float)ua <= alpha;
+        if (acc) lt = lt_p;
+#else
+        const double hast = tn_logZ(oh, mh->sl, mh->lb_h, mh->ub_h) -
+                            tn_logZ(nh, mh->sl, mh->lb_h, mh->ub_h) +
+                            tn_logZ(ow, mh->sl, mh->lb_w, mh->ub_w) -
+                            tn_logZ(nw, mh->sl, mh->lb_w, mh->ub_w) +
+                            tn_logZ(of, mh->sf, mh->lb_f, mh->ub_f) -
+                            tn_logZ(nf, mh->sf, mh->lb_f, mh->ub_f);
+        const double dprior = (j < cnt) ? -(pr->alpha + 1) * (log(nf) - log(of)) : 0.0;
+        const double loga = dprior + tau[t] * (nll - ll) + hast;
+        const double e = exp(loga);
+        const double alpha = e > 1.0 ? 1.0 : e;
+        acc = ua <= alpha;
+#endif
+        if (acc) {
+          ll = nll;
+          ws_accept(m, &ws, j, &wj, bb);
+        } else {
+          ws.h[j] = oh;
+          ws.w[j] = ow;
+          ws.f[j] = of;
+        }
+      }
+      for (int s = 0; s < S; ++s) {
+        locs[(pid * S + s) * 2 + 0] = (float)ws.h[s];
+        locs[(pid * S + s) * 2 + 1] = (float)ws.w[s];
+        fluxes[pid * S + s] = (float)ws.f[s];
+      }
+      if (acc_last) acc_last[pid] = (uint8_t)acc;
+    }
+    ws_free(&ws);
+  }
+  return 0;
+}
+
+/* image log-likelihoods of T*N particles in `real` arithmetic (float64
+ * build: = mh_oracle_loglik bit for bit) */
+int mh_oracle_loglik_cached(const om_model_t* m, const float* image, const float* locs,
+                            const float* fluxes, int T, int N, int S, int threads, double* out) {
+  const int HW = m->H * m->W;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#endif
+#pragma omp parallel
+  {
+    om_ws_t ws;
+    ws_alloc(&ws, m, S);
+#pragma omp for schedule(static)
+    for (long pid = 0; pid < (long)T * N; ++pid) {
+      const float* x = image + (size_t)(pid / N) * HW;
+      for (int p = 0; p < HW; ++p) ws.lgx[p] = (real)lgamma((double)x[p] + 1.0);
+      for (int s = 0; s < S; ++s) {
+        ws.h[s] = locs[(pid * S + s) * 2 + 0];
+        ws.w[s] = locs[(pid * S + s) * 2 + 1];
+        ws.f[s] = fluxes[pid * S + s];
+      }
+      out[pid] = ws_render(m, &ws, x);
+    }
+    ws_free(&ws);
   }
   return 0;
 }
