@@ -54,6 +54,8 @@ F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
 # FETCH_SIZE / WRITE_SIZE (HBM traffic), SQ VALU counts, GRBM_GUI_ACTIVE (effective clock),
 # and the sha1 of the library sources it was measured on
 PMC_FILE = "pmc_mh_r04.json"
+# the same for the C4 / C5 MH launches (the default run's `c4` / `c5` legs)
+PMC_FILES = {"c2": PMC_FILE, "c4": "pmc_mh_c4_r05.json", "c5": "pmc_mh_c5_r05.json"}
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions/s: 1 per SIMD per 4 cycles (measured 4.2)
 # measured SIMD issue cycles per wave-instruction (scripts/probe/isa_probe.hip, 4 waves/SIMD,
 # profiles/r01_s2_isa_probe.txt): plain VALU 4.2, transcendental 8.6, packed f32 6.0
@@ -162,6 +164,8 @@ def parse():
     ap.add_argument("--no-c3", action="store_true")
     # skip the untimed step-spread passes
     ap.add_argument("--no-spread", action="store_true")
+    # skip the C4 / C5 / C3-rank-share legs of the default C2 run
+    ap.add_argument("--no-legs", action="store_true")
     # diagnostic MH flags (A/B timing: e.g. 2048 = SMCDET_MH_NO_PSF_CACHE)
     ap.add_argument("--mh-debug-flags", type=int, default=0)
     # CPU rehearsal of the multi-rank bookkeeping (gloo, RehearsalSampler: no
@@ -511,13 +515,16 @@ def pmc_summary(args):
     """The committed PMC summary of the C2 MH launch, or (None, reason).  A
     summary measured on other library sources than the loaded library's is
     stale: its counters do not describe this run's kernel."""
-    if args.workload != "c2" or args.kernel != "mh" or args.full_recompute:
+    fname = PMC_FILES.get(args.workload)
+    if fname is None or args.kernel != "mh" or args.full_recompute:
         return None, "no PMC summary for this workload"
     if REHEARSAL:
         return None, "host rehearsal (no kernel)"
-    path = os.path.join(ROOT, "profiles", PMC_FILE)
+    if args.workload == "c2" and (args.total_tiles > 0 or args.tiles_per_gpu != 1):
+        return None, "no PMC summary for this tile count"
+    path = os.path.join(ROOT, "profiles", fname)
     if not os.path.exists(path):
-        return None, f"profiles/{PMC_FILE} missing"
+        return None, f"profiles/{fname} missing"
     try:
         d = json.load(open(path))
     except Exception as e:  # never fail the bench line on it
@@ -525,9 +532,9 @@ def pmc_summary(args):
     from smcdet_amd import _hip
     built = _hip.built_hash()
     if d.get("source_hash") != built:
-        return None, (f"stale: profiles/{PMC_FILE} was measured on library sources "
+        return None, (f"stale: profiles/{fname} was measured on library sources "
                       f"{d.get('source_hash')}, this library is {built}")
-    return d, f"profiles/{PMC_FILE}"
+    return d, f"profiles/{fname}"
 
 
 def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
@@ -720,6 +727,85 @@ def c3_leg(args, dev, rank, world, dist, backend):
             "catalog_gather": gather}
 
 
+def workload_leg(args, dev, rank, world, dist, backend, name):
+    """The other BASELINE configurations riding along the default C2 run,
+    each a timed SMC step on resident data like the main line (warm-up,
+    barrier + synchronize on both sides, MAX over ranks), plus the MH launch's
+    own duration (dispatch-stamped HIP events, untimed pass) and its roofline:
+      c4             configs[3]: 42 8x8 M71 cutouts per GPU (332 over 8 GPUs,
+                     manuscript.tex:562), S=10, N=4096, K=100, batched;
+      c5             configs[4]: CS-SMC over the same 42 cutouts, counts 0..6,
+                     N=8192 per count;
+      c3_rank_share  one rank's share of configs[2] on 8 GPUs: tiles 0..7 of
+                     the 64 (seeds 1000..1007, distributed.shard_tiles(64, 8, 0)),
+                     so 8 x its rate projects the 8-GPU C3 line (world 1 only)."""
+    import argparse as _ap
+    import torch.distributed as tdist
+    from smcdet_amd import _hip
+    a2 = _ap.Namespace(**vars(args))
+    if name == "c3_rank_share":
+        a2.workload, a2.total_tiles, a2.tiles_per_gpu = "c2", 8, 1
+    else:
+        a2.workload, a2.total_tiles, a2.tiles_per_gpu = name, 0, 42
+    s, _, steps_per_step, _, cfg = build_sampler(a2, dev, rank)
+    s.fused_step = False
+    s.initialize()
+    s._temper_reweight(with_resample=True)
+
+    def step():
+        idx, s._pending_idx = s._pending_idx, None
+        s._step(idx)
+
+    steps = max(3, min(args.steps, 10))
+    for _ in range(2):
+        step()
+    _sync()
+    if dist:
+        tdist.barrier()
+    _sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    _sync()
+    if dist:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu",
+                         dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t)
+    _hip.launch_timing(steps)
+    for _ in range(steps):
+        step()
+    _sync()
+    ev = _hip.launch_timing_read(steps)
+    _hip.launch_timing(0)
+    mh_ms = sum(ev) / max(len(ev), 1)
+    S_, HW_ = cfg["sources"], cfg["tile"] * cfg["tile"]
+    b_alg = 24 * S_ + 8
+    f_alg = S_ * min(289, HW_) * 20 + HW_ * 10
+    mh_rate = steps_per_step / (mh_ms * 1e-3)
+    out = {"value": (world if name != "c3_rank_share" else 1) * steps_per_step * steps / elapsed,
+           "unit": "particle-steps/sec", "n_gpus": world if name != "c3_rank_share" else 1,
+           "steps": steps, "warmup": 2, "ms_per_step": elapsed / steps * 1e3,
+           "scaling": "weak", "config": cfg, "kernel_ms": mh_ms,
+           "mh_particle_steps_per_launch": steps_per_step,
+           "roofline": {"bound": "hbm", "achieved": b_alg * mh_rate / 1e9, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": b_alg * mh_rate / 1e9 / HBM_PEAK_GBS,
+                        "alg_bytes_per_particle_step": b_alg,
+                        "kernel_timing": f"HIP dispatch events, {len(ev)} launches"}}
+    pmc, _ = pmc_summary(a2)
+    out["roofline"]["traffic"] = pmc.get("hbm_bytes_per_launch") if pmc else None
+    out["compute"] = compute_block(a2, mh_rate, f_alg, steps_per_step, mh_ms)
+    if name == "c3_rank_share":
+        out["projected_8gpu_c3_value"] = 8 * out["value"]
+        out["note"] = ("one rank's share (8 tiles) of the 64-tile C3 split at 8 GPUs, run on "
+                       "this GPU alone; the 8-GPU figure is 8 x this rate (ranks share no "
+                       "data path), a projection, not a measurement")
+    return out
+
+
 def catalog_gather(s, rank, world, dist, backend):
     """north_star's one collective: the end-of-run catalog gather of every
     rank's tiles (smcdet_amd.distributed.gather_tile_results: one gather to
@@ -873,6 +959,15 @@ def main():
             and args.tiles_per_gpu == 1 and not args.no_c3 and world <= C3_TILES):
         c3 = c3_leg(args, dev, rank, world, dist, backend)
 
+    legs = {}
+    if (args.workload == "c2" and args.kernel == "mh" and args.total_tiles == 0
+            and args.tiles_per_gpu == 1 and not args.no_legs and not REHEARSAL):
+        for name in ("c4", "c5") + (("c3_rank_share",) if world == 1 else ()):
+            try:
+                legs[name] = workload_leg(args, dev, rank, world, dist, backend, name)
+            except Exception as e:  # report, never fail the bench line on it
+                legs[name] = {"error": repr(e)}
+
     if args.total_tiles > 0:  # strong scaling: every rank's tiles, uneven shares included
         value = args.total_tiles * args.particles * args.mh_iters * args.steps / elapsed
     else:
@@ -938,6 +1033,7 @@ def main():
                 "intervals and durations from the dispatch-stamped timing pass"}
     if c3 is not None:
         out["c3_strong"] = c3
+    out.update(legs)
     # SURVEY §8d also asks for the wall time to temperature 1: one complete
     # run() (initialise, SMC loop with its per-iteration stopping check, final
     # resample, prune) on a fresh sampler, outside the timed region

@@ -31,7 +31,7 @@ VARIANTS = {
     "default": {},
     "no_persist": {"persist_rate_images": False},
     "full": {"full_recompute": True},
-    "unfused": {"fused": False},
+    "unfused": {"fused": False, "stopping": "lockstep"},
     "refresh1": {"rate_refresh_every": 1},
 }
 
@@ -56,7 +56,7 @@ def run(which, n_runs, variant, seed=777):
     s = SMCsampler.from_tiles(tiles, prior, model, mh, N, cfg["rho"], cfg["method"],
                               p["flux_detection_threshold"], cfg.get("max_smc_iters", 1000),
                               print_every=10 ** 9, seed=seed, device=dev,
-                              stopping="independent", **v)
+                              **dict({"stopping": "independent"}, **v))
     t0 = time.perf_counter()
     with contextlib.redirect_stdout(io.StringIO()):
         s.run()

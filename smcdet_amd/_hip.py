@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes
 import functools
 import os
+import threading
 
 import torch
 
@@ -235,8 +236,13 @@ class _Checked:
         self._fn, self._name = fn, name
 
     def __call__(self, *args):
-        check_aliases(self._name, args)
-        return self._fn(*args)
+        try:
+            check_aliases(self._name, args)
+            return self._fn(*args)
+        finally:
+            # the launch is enqueued: the argument temporaries ptr() kept may
+            # go (their blocks are reused in stream order, after the launch)
+            _release_kept()
 
     def __getattr__(self, k):
         return getattr(self._fn, k)
@@ -253,7 +259,14 @@ class _Lib:
                 setattr(self, name, _Checked(getattr(cdll, name), name))
 
     def __getattr__(self, k):
-        return getattr(self._cdll, k)
+        # every other entry point also releases ptr()'s temporaries after the
+        # call (check_aliases has no spec for it and returns at once)
+        fn = getattr(self._cdll, k)
+        if k.startswith("smcdet_") and callable(fn):
+            w = _Checked(fn, k)
+            setattr(self, k, w)
+            return w
+        return fn
 
 
 _lib = None
@@ -375,20 +388,36 @@ def launch_timing_starts(max_launches: int):
     return [float(buf[i]) for i in range(min(n.value, int(max_launches)))]
 
 
-# ptr() keeps the last _KEEP tensors it converted alive, so a temporary passed
-# as `ptr(torch.tensor(...))` outlives the call it is an argument of (and its
-# block cannot be handed to the next temporary of the same call)
-_KEEP = 256
-_kept = [None] * _KEEP
-_kept_i = 0
+# ptr() keeps the tensors it converts alive until the next library call made
+# through lib() returns (per thread), so a temporary passed as
+# `ptr(torch.tensor(...))` outlives the call it is an argument of -- its block
+# cannot be handed to the next temporary of the same argument list -- and is
+# released right after that call: no step's buffers are held beyond it.
+# _KEEP_MAX bounds the list for code that converts without calling.
+_KEEP_MAX = 4096
+_tls = threading.local()
+
+
+def _kept():
+    k = getattr(_tls, "kept", None)
+    if k is None:
+        k = _tls.kept = []
+    return k
+
+
+def _release_kept():
+    k = getattr(_tls, "kept", None)
+    if k:
+        k.clear()
 
 
 def ptr(t):
-    global _kept_i
     if t is None:
         return None
-    _kept[_kept_i] = t
-    _kept_i = (_kept_i + 1) % _KEEP
+    k = _kept()
+    if len(k) >= _KEEP_MAX:
+        del k[:_KEEP_MAX // 2]
+    k.append(t)
     return ctypes.c_void_p(t.data_ptr())
 
 

@@ -55,6 +55,11 @@ class SMCsampler(object):
                           self._particles_per_tile(Prior, num_catalogs), nt,
                           getattr(ImageModel, "psf_radius", None), where="SMCsampler",
                           global_ok=global_ok)
+        if stopping == "independent" and not fused:
+            # the method-by-method schedule (resample / mutate / temper /
+            # update_weights, fused=False) is the reference's lockstep loop;
+            # freezing finished tiles lives in the fused step's kernels
+            raise ValueError("stopping='independent' needs the fused schedule (fused=True)")
         if device is None:
             device = image.device if image.is_cuda else torch.device(
                 "cuda", torch.cuda.current_device())
@@ -594,8 +599,6 @@ class SMCsampler(object):
         if self.fused:
             self._temper_reweight(with_resample=True)
         else:
-            if self.stopping != "lockstep":
-                raise NotImplementedError("independent stopping runs on the fused schedule")
             self.temper()
             self.update_weights()
         self._loop()

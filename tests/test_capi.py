@@ -153,3 +153,34 @@ def test_ptr_keeps_temporaries_alive():
     del t
     gc.collect()
     assert r() is not None and p.value == addr
+
+
+def test_ptr_temporaries_released_after_the_call():
+    """ptr()'s temporaries live until the library call they are
+    arguments of returns, and no longer (no step's buffers are held across
+    steps); many steps' worth of conversions stay bounded."""
+    import gc
+    import weakref
+
+    import torch
+
+    from smcdet_amd import _hip
+    L = _hip.lib()
+    refs = []
+    for _ in range(300):  # > the old 256-entry ring
+        t = torch.empty(8)
+        refs.append(weakref.ref(t))
+        _hip.ptr(t)
+        del t
+        gc.collect()
+        assert refs[-1]() is not None  # alive until a call
+        L.smcdet_launch_timing(0)        # any entry point (no GPU work)
+        gc.collect()
+        assert refs[-1]() is None        # released once the call returned
+    assert all(r() is None for r in refs)
+    # the bound for conversions that never reach a call
+    for _ in range(_hip._KEEP_MAX + 10):
+        _hip.ptr(torch.empty(1))
+    assert len(_hip._kept()) <= _hip._KEEP_MAX
+    L.smcdet_launch_timing(0)
+    assert len(_hip._kept()) == 0

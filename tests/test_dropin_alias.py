@@ -105,6 +105,11 @@ def test_unsupported_shapes_fail_at_construction():
     model, prior = make(32, 10)
     with pytest.raises(ValueError, match="20000 particles per tile > 16384"):
         SMCsampler(torch.zeros(32, 32), 32, prior, model, mh, 20000, 0.5, "systematic", 0.25, 10)
+    # independent stopping lives in the fused step's
+    # kernels; the method-by-method schedule refuses it at construction
+    with pytest.raises(ValueError, match="independent.*fused"):
+        SMCsampler(torch.zeros(32, 32), 32, prior, model, mh, 512, 0.5, "systematic", 0.25, 10,
+                   fused=False, stopping="independent")
 
 
 def test_struct_caches_follow_rebinding():

@@ -195,17 +195,22 @@ def test_c5_full_size_cssmc():
     np.testing.assert_array_equal(cs.counts[0].cpu().numpy(), k.astype(np.float32))
 
 
-def test_c5_statistical_vs_reference():
-    ref = _load("stats_c5.json")
+def test_c5_statistical_vs_oracle():
+    """C5 against the oracle's CS-SMC target (tests/golden/stats_c5_oracle.json,
+    make_oracle_stats.py run_c5: >= 48 runs of the float64 restatement of the
+    reference's fixed-count samplers on the stats_c5.json cutout).  Gates fixed
+    before the target was generated: per-count log Z within
+    3 pooled SE and 1% for every s >= 1, no exemption; p(s|x) within 3 pooled
+    SE for every s, no slack (a 1e-6 floor for strata whose posterior is 0
+    to float precision).  256 GPU runs of the cutout in one sampler."""
+    ref = _load("stats_c5_oracle.json")
     rr = ref["runs"]
-    if len(rr) < 8:
-        # (a reference C5 run is 7 fixed-count samplers at N = 8192: ~100 min
-        # on this container's CPU, so the set grows slowly)
-        pytest.skip(f"stats_c5.json: {len(rr)} reference runs (< 8)")
+    if len(rr) < 48:
+        pytest.skip(f"stats_c5_oracle.json: {len(rr)} oracle runs (< 48)")
     cfg = ref["config"]
     assert (cfg["N"], cfg["K"], cfg["smax"]) == (8192, 100, 6)
     img = torch.tensor(ref["image"], dtype=torch.float32, device=DEV)
-    n = 24
+    n = 256
     cs = _c5(img[None].expand(n, H, H).contiguous(), 99)
     cs.run()
     lz = cs.log_normalizing_constant_per_count[0].double().cpu().numpy()   # [n, 7]
@@ -213,17 +218,37 @@ def test_c5_statistical_vs_reference():
     rl = np.array([x["logZ"] for x in rr])
     rp = np.array([x["count_posterior"] for x in rr])
     np.testing.assert_allclose(lz[:, 0], cfg["loglik_empty"], rtol=1e-5)
+    fails = []
     for s in range(1, 7):
         d = lz[:, s].mean() - rl[:, s].mean()
-        print("C5 count", s, "log Z", lz[:, s].mean(), "+-", _se(lz[:, s], rl[:, s]), "ref",
-              rl[:, s].mean())
         se_s = _se(lz[:, s], rl[:, s])
-        assert abs(d) <= 3 * se_s + 1e-3, (s, lz[:, s].mean(), rl[:, s].mean())
-        # the 1% bound where the stratum's evidence is well determined; a
-        # multi-modal stratum (count 2 of this cutout: the reference's own
-        # runs spread 37 nats) is held to the 3-SE bound alone
-        if se_s < 0.005 * abs(rl[:, s].mean()):
-            assert abs(d) <= 0.01 * abs(rl[:, s].mean()), (s, lz[:, s].mean(), rl[:, s].mean())
+        print(f"C5 count {s}: log Z {lz[:, s].mean():.2f} (sd {lz[:, s].std():.2f}) oracle "
+              f"{rl[:, s].mean():.2f} (sd {rl[:, s].std():.2f}); diff {d:+.2f}, pooled SE "
+              f"{se_s:.2f}, 1% {0.01 * abs(rl[:, s].mean()):.2f}")
+        if abs(d) > 3 * se_s or abs(d) > 0.01 * abs(rl[:, s].mean()):
+            fails.append(s)
     se = np.sqrt(post.var(0, ddof=1) / len(post) + rp.var(0, ddof=1) / len(rp))
-    print("C5 p(s|x)", post.mean(0).round(3), "ref", rp.mean(0).round(3))
-    assert np.all(np.abs(post.mean(0) - rp.mean(0)) <= 3 * se + 0.02), (post.mean(0), rp.mean(0))
+    print("C5 p(s|x)", post.mean(0).round(3), "oracle", rp.mean(0).round(3), "SE", se.round(3))
+    assert not fails, fails
+    assert np.all(np.abs(post.mean(0) - rp.mean(0)) <= 3 * se + 1e-6), (post.mean(0), rp.mean(0))
+
+
+def test_c5_reference_smoke():
+    """The 8 reference CS-SMC runs (stats_c5.json, ~100 min each on the CPU)
+    cannot resolve 1% at any count; against them the GPU's per-count medians
+    must lie within the reference runs' range, and log Z_0 is the reference's
+    empty-catalog likelihood.  The 1% gate is test_c5_statistical_vs_oracle's,
+    and the oracle target's agreement with these runs is
+    tests/test_oracle_targets.py's."""
+    ref = _load("stats_c5.json")
+    rr = ref["runs"]
+    cfg = ref["config"]
+    img = torch.tensor(ref["image"], dtype=torch.float32, device=DEV)
+    cs = _c5(img[None].expand(24, H, H).contiguous(), 98)
+    cs.run()
+    lz = cs.log_normalizing_constant_per_count[0].double().cpu().numpy()
+    rl = np.array([x["logZ"] for x in rr])
+    np.testing.assert_allclose(lz[:, 0], cfg["loglik_empty"], rtol=1e-5)
+    for s in range(1, 7):
+        med = np.median(lz[:, s])
+        assert rl[:, s].min() - 1.0 <= med <= rl[:, s].max() + 1.0, (s, med, rl[:, s])

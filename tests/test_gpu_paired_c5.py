@@ -1,0 +1,204 @@
+"""Paired (same-draws) count-stratified runs at C5 (VERDICT r4 "next" #1):
+the stats_c5.json cutout (8x8 M71), counts 0..6, N = 8192 per count, K = 100,
+rho = 0.5, systematic (manuscript.tex:322-356, :566, :648).
+
+tests/golden/stats_c5_oracle.json holds complete CS-SMC runs of the CPU
+restatement (tests/golden/make_oracle_stats.py run_c5: for each count
+s = 1..6 a fixed-count run of the float64 C sweep with S = s, brentq
+tempering, softmax reweighting, systematic resampling -- the reference's loop
+smcdet/sampler.py:221-256 with smcdet/kernel.py:26-130 -- with numpy PCG64
+streams seeded 1000*seed + s and splitmix64 sweeps).  Here the GPU's
+CountStratifiedSMC (all seven strata as the stratum tiles of one sampler,
+padded to S = 6, the moved component drawn from 0..count-1) replays exactly
+those draws: each stratum's prior uniforms, systematic offsets and every MH
+draw (oracle.c_oracle.sweep_draws), so every GPU stratum is its oracle
+stratum's twin until a float32 decision differs from the float64 one.
+
+Gates (fixed before the target was generated):
+  * pairing: ladders equal (|delta tau| <= 1e-5) for the first two
+    iterations in >= 90% of the stratum runs with s >= 1;
+  * per count s >= 1, the paired differences d = log Z_gpu - log Z_oracle:
+    |mean d| <= 3 SE(d) and |mean d| <= 1% of |mean log Z_oracle|;
+  * p(s|x): paired mean difference within 3 SE for every s (no slack; a
+    1e-6 floor for the strata whose posterior is 0 to float precision);
+  * the winning count (argmax_s log p(s) + log Z_s): for every s, an exact
+    McNemar test of "wins here only" vs "wins in the oracle only",
+    two-sided p > 0.002 (0.01 / 7 strata, rounded).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests._params import GOLDEN, M71, p_m71_mh, p_m71_model, p_m71_prior
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+TARGET = "stats_c5_oracle.json"
+MIN_RUNS = 48
+CHUNKS = 8
+_results = {}
+
+
+def _target():
+    path = os.path.join(GOLDEN, TARGET)
+    if not os.path.exists(path):
+        pytest.skip(f"{TARGET} not generated")
+    with open(path) as f:
+        doc = json.load(f)
+    if len(doc["runs"]) < MIN_RUNS:
+        pytest.skip(f"{TARGET}: {len(doc['runs'])} oracle runs (< {MIN_RUNS})")
+    doc["runs"] = doc["runs"][:MIN_RUNS] if os.environ.get("SMCDET_PAIRED_C5_ALL") is None \
+        else doc["runs"]
+    return doc
+
+
+def paired_c5_run(img, cfg, seed):
+    """make_oracle_stats.run_c5's strata, streams and schedule on the GPU's
+    count-stratified sampler.  Returns per-count log Z, iterations and
+    temperature ladders."""
+    from oracle import c_oracle as C
+    from smcdet_amd.cssmc import CountStratifiedSMC
+    H, N, K, smax = cfg["tile"], cfg["N"], cfg["K"], cfg["smax"]
+    NS = smax + 1
+    image = torch.tensor(img, dtype=torch.float32, device=DEV).reshape(1, 1, H, H)
+    mh = p_m71_mh(K)
+    cs = CountStratifiedSMC(image, H, p_m71_prior(H, 0, smax), p_m71_model(H), mh, N, cfg["rho"],
+                            "systematic", M71["flux_detection_threshold"], 100,
+                            print_every=10 ** 9, seed=seed, device=DEV)
+    s = cs.sampler
+    kern = cs.MutationKernel
+    counts = torch.zeros(1, NS, N, device=DEV)
+    locs = torch.zeros(1, NS, N, smax, 2, device=DEV)
+    fluxes = torch.zeros(1, NS, N, smax, device=DEV)
+    rngs = [None] + [np.random.default_rng(1000 * seed + k) for k in range(1, NS)]
+    for k in range(1, NS):
+        uloc = torch.from_numpy(rngs[k].random((1, 1, N, k, 2), dtype=np.float32))
+        uflux = torch.from_numpy(rngs[k].random((1, 1, N, k), dtype=np.float32))
+        c, lo, f = p_m71_prior(H, k, k).sample_stratified(1, N, device=DEV, uloc=uloc,
+                                                          uflux=uflux)
+        counts[0, k] = c[0, 0]
+        locs[0, k, :, :k] = lo[0, 0]
+        fluxes[0, k, :, :k] = f[0, 0]
+    s.counts, s.locs, s.fluxes = counts, locs, fluxes
+    s.temperature_prev = torch.zeros(1, NS, device=DEV)
+    s.temperature = torch.zeros(1, NS, device=DEV)
+    s.log_normalizing_constant = torch.zeros(1, NS, device=DEV)
+    s._fresh_loglik = None
+    s.temper()
+    s.update_weights()
+    s.iter = 0
+    taus = [s.temperature.flatten().cpu().numpy().copy()]
+    mask = 0xFFFFFFFFFFFF
+    while bool((s.temperature < 1).any()) and s.iter <= s.max_smc_iters:
+        s.iter += 1
+        u = np.full((1, NS), 0.5, np.float32)
+        for k in range(1, NS):
+            u[0, k] = rngs[k].random((1, 1), dtype=np.float32)[0, 0]
+        idx = s.resample_index(u=torch.from_numpy(u))
+        comp = np.zeros((K, 1, NS, N), np.int32)
+        ul = np.zeros((K, 1, NS, N, 2), np.float32)
+        uf = np.zeros((K, 1, NS, N), np.float32)
+        ua = np.zeros((K, 1, NS, N), np.float32)
+        done = (s.temperature.flatten() >= 1).cpu().numpy()
+        for k in range(1, NS):
+            if done[k]:
+                # a finished stratum's log Z is final: its particles stay put
+                # (log U = +inf rejects every proposal)
+                ua[:, 0, k] = np.inf
+                continue
+            d = C.sweep_draws(((1000 * seed + k) * 1000003 + s.iter) & mask, 1, N, K, k)
+            comp[:, 0, k], ul[:, 0, k] = d["comp"][:, 0], d["uloc"][:, 0]
+            uf[:, 0, k], ua[:, 0, k] = d["uflux"][:, 0], d["uacc"][:, 0]
+        replay = {"comp": torch.from_numpy(comp), "uloc": torch.from_numpy(ul),
+                  "uflux": torch.from_numpy(uf), "uacc": torch.from_numpy(ua)}
+        s.locs, s.fluxes, s.mutation_acc_rates = kern.run(
+            s.tiled_image, s.counts, s.locs, s.fluxes, s.temperature, s.log_target,
+            ancestors=idx, replay=replay)
+        s.counts = kern.last_counts
+        s._fresh_loglik = kern.last_loglik
+        s.temper()
+        s.update_weights()
+        taus.append(s.temperature.flatten().cpu().numpy().copy())
+    lz = s.log_normalizing_constant.flatten().double().cpu().numpy()
+    v = lz + np.array(cfg["log_count_prior"])
+    p = np.exp(v - v.max())
+    taus = np.stack(taus)  # [iters+1, NS]
+    return dict(seed=seed, logZ=lz.tolist(), count_posterior=(p / p.sum()).tolist(),
+                tau=[taus[:, k].tolist() for k in range(NS)])
+
+
+@pytest.mark.parametrize("chunk", range(CHUNKS))
+def test_paired_c5_chunk(chunk):
+    ref = _target()
+    for r in ref["runs"][chunk::CHUNKS]:
+        out = paired_c5_run(ref["image"], ref["config"], r["seed"])
+        first = []
+        for k in range(1, len(out["logZ"])):
+            ot, gt = r["tau_trace"][k], out["tau"][k]
+            n = min(len(ot), len(gt))
+            off = [i for i in range(n) if abs(ot[i] - gt[i]) > 1e-5]
+            first.append(off[0] if off else n)
+        out["first_tau_divergence"] = first
+        _results[r["seed"]] = out
+        print(f"seed {r['seed']}: GPU log Z {np.round(out['logZ'][1:], 2).tolist()} oracle "
+              f"{np.round(r['logZ'][1:], 2).tolist()} ladders part at {first}", flush=True)
+
+
+def _mcnemar_p(b, c):
+    from math import comb
+    n, k = b + c, min(b, c)
+    if n == 0:
+        return 1.0
+    return min(1.0, 2.0 * sum(comb(n, i) for i in range(k + 1)) / 2.0 ** n)
+
+
+def test_paired_c5_gates():
+    ref = _target()
+    runs = ref["runs"]
+    if any(r["seed"] not in _results for r in runs):
+        pytest.skip("needs every chunk of test_paired_c5_chunk")
+    res = [_results[r["seed"]] for r in runs]
+    lz = np.array([x["logZ"] for x in res])
+    lz_o = np.array([r["logZ"] for r in runs])
+    p = np.array([x["count_posterior"] for x in res])
+    p_o = np.array([r["count_posterior"] for r in runs])
+    first = np.array([x["first_tau_divergence"] for x in res])  # [runs, 6]
+    n = len(res)
+    summary = {"n": n, "ladder_share_ge_2": float((first >= 2).mean()),
+               "ladder_first_divergence_median": float(np.median(first)), "per_count": {}}
+    fails = []
+    if (first >= 2).mean() < 0.9:
+        fails.append("pairing")
+    for s in range(1, lz.shape[1]):
+        d = lz[:, s] - lz_o[:, s]
+        se = d.std(ddof=1) / np.sqrt(n)
+        one = 0.01 * abs(lz_o[:, s].mean())
+        row = dict(gpu=lz[:, s].mean(), oracle=lz_o[:, s].mean(), mean_d=d.mean(), se_d=se,
+                   one_pct=one, median_abs_d=float(np.median(np.abs(d))))
+        summary["per_count"][s] = row
+        if abs(d.mean()) > 3 * se or abs(d.mean()) > one:
+            fails.append(f"log Z count {s}")
+    dp = p - p_o
+    se_p = dp.std(0, ddof=1) / np.sqrt(n)
+    summary["posterior"] = dict(gpu=p.mean(0).round(4).tolist(), oracle=p_o.mean(0).round(4).tolist(),
+                                se=se_p.round(4).tolist())
+    if np.any(np.abs(dp.mean(0)) > 3 * se_p + 1e-6):
+        fails.append("p(s|x)")
+    win, win_o = p.argmax(1), p_o.argmax(1)
+    summary["same_winner"] = int((win == win_o).sum())
+    mc = {}
+    for s in range(lz.shape[1]):
+        b, c = int(((win == s) & (win_o != s)).sum()), int(((win != s) & (win_o == s)).sum())
+        mc[s] = (b, c, _mcnemar_p(b, c))
+        if mc[s][2] <= 0.002:
+            fails.append(f"winner count {s}")
+    summary["winner_mcnemar"] = mc
+    path = os.environ.get("SMCDET_PAIRED_C5_OUT")
+    if path:
+        with open(path, "w") as f:
+            json.dump(dict(summary, runs=res), f, indent=1, default=float)
+    print(json.dumps(summary, indent=1, default=float))
+    assert not fails, (fails, summary)
