@@ -404,35 +404,30 @@ __device__ __forceinline__ f2 psf_raw2(const DevModel& m, f2 r2) {
 // lanes' scattered b128 reads made the 32x32 sweep 50% slower.
 // The index comes from the float32 round-to-nearest trick: y = u + 1.5*2^23
 // holds round(u) in its low mantissa bits (u < 2^22), y - 1.5*2^23 is that
-// integer exactly, so t is exact too.  CLAMP bounds the index for positions
-// outside the source's window (union windows of moved anchors: their value is
-// discarded, only the LDS address must stay inside the table).
+// integer exactly, so t is exact too.  The index is clamped to the last node
+// in every use: positions outside the source's window (union windows of moved
+// anchors, masked lanes' dummy positions) have their value discarded, but the
+// LDS address must stay inside the table.
 // ---------------------------------------------------------------------------
 constexpr int kTabIntervals = 512;
 constexpr int kTabNodes = kTabIntervals + 1;
 constexpr float kRoundMagic = 12582912.0f;  // 1.5 * 2^23
 constexpr int kRoundMagicBits = 0x4B400000;
 
-template <bool CLAMP>
 __device__ __forceinline__ float psf_tab(const float4* tab, float inv_h, float r2) {
   const float u = r2 * inv_h;
   const float y = u + kRoundMagic;
   const float t = u - (y - kRoundMagic);
-  int i = __float_as_int(y) - kRoundMagicBits;
-  if (CLAMP) i = min(i, kTabIntervals);
+  const int i = min(__float_as_int(y) - kRoundMagicBits, kTabIntervals);
   const float4 c = tab[i];
   return fmaf(fmaf(fmaf(c.w, t, c.z), t, c.y), t, c.x);
 }
-template <bool CLAMP>
 __device__ __forceinline__ f2 psf_tab2(const float4* tab, float inv_h, f2 r2) {
   const f2 u = r2 * inv_h;
   const f2 y = u + kRoundMagic;
   const f2 t = u - (y - kRoundMagic);
-  int i0 = __float_as_int(y.x) - kRoundMagicBits, i1 = __float_as_int(y.y) - kRoundMagicBits;
-  if (CLAMP) {
-    i0 = min(i0, kTabIntervals);
-    i1 = min(i1, kTabIntervals);
-  }
+  const int i0 = min(__float_as_int(y.x) - kRoundMagicBits, kTabIntervals);
+  const int i1 = min(__float_as_int(y.y) - kRoundMagicBits, kTabIntervals);
   const float4 c0 = tab[i0], c1 = tab[i1];
   return f2{fmaf(fmaf(fmaf(c0.w, t.x, c0.z), t.x, c0.y), t.x, c0.x),
             fmaf(fmaf(fmaf(c1.w, t.y, c1.z), t.y, c1.y), t.y, c1.x)};

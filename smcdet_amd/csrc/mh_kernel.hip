@@ -175,8 +175,8 @@ __device__ __forceinline__ float position_delta(const DevModel& m, const float* 
   const float dhn = fph - P.hn, dwn = fpw - P.wn;
   float psi_o, psi_n;
   if constexpr (TB) {
-    psi_o = psf_tab<WINDOWS>(tab, tinv, fmaf(dho, dho, dwo * dwo));
-    psi_n = psf_tab<WINDOWS>(tab, tinv, fmaf(dhn, dhn, dwn * dwn));
+    psi_o = psf_tab(tab, tinv, fmaf(dho, dho, dwo * dwo));
+    psi_n = psf_tab(tab, tinv, fmaf(dhn, dhn, dwn * dwn));
   } else {
     psi_o = psf_raw<MODEL>(m, fmaf(dho, dho, dwo * dwo));
     psi_n = psf_raw<MODEL>(m, fmaf(dhn, dhn, dwn * dwn));
@@ -220,8 +220,8 @@ __device__ __forceinline__ f2 position_delta2(const DevModel& m, const float* xs
   const f2 dhn = fph - P.hn, dwn = fpw - P.wn;
   f2 psi_o, psi_n;
   if constexpr (TB) {
-    psi_o = psf_tab2<WINDOWS>(tab, tinv, fma2(dho, dho, dwo * dwo));
-    psi_n = psf_tab2<WINDOWS>(tab, tinv, fma2(dhn, dhn, dwn * dwn));
+    psi_o = psf_tab2(tab, tinv, fma2(dho, dho, dwo * dwo));
+    psi_n = psf_tab2(tab, tinv, fma2(dhn, dhn, dwn * dwn));
   } else {
     psi_o = psf_raw2<MODEL>(m, fma2(dho, dho, dwo * dwo));
     psi_n = psf_raw2<MODEL>(m, fma2(dhn, dhn, dwn * dwn));
@@ -280,7 +280,7 @@ __device__ __forceinline__ float position_delta_pc(const DevModel& m, const floa
   const float dhn = fph - P.hn, dwn = fpw - P.wn;
   const float psi_o = pcj[valid ? p : 0];  // (a masked lane's value is discarded)
   float psi_n;
-  if constexpr (TB) psi_n = psf_tab<WINDOWS>(tab, tinv, fmaf(dhn, dhn, dwn * dwn));
+  if constexpr (TB) psi_n = psf_tab(tab, tinv, fmaf(dhn, dhn, dwn * dwn));
   else psi_n = psf_raw<MODEL>(m, fmaf(dhn, dhn, dwn * dwn));
   if (WINDOWS) {
     const unsigned span = 2u * (unsigned)m.R;
@@ -397,7 +397,8 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
   static_assert(!TB || (MODEL == SMCDET_MODEL_M71 && PPL > 0 && !FULL && !GL && !TAIL && PAIRED),
                 "PSF table: M71 register-render tiles, incremental, paired");
   constexpr int NSL = mh_slots<PPL>();
-  extern __shared__ float smem[];
+  // 16-byte aligned: the PSF table (TB) is read as float4 at smem + offset
+  extern __shared__ __align__(16) float smem[];
   __shared__ int wg_acc, wg_done;  // last-iteration accepts / finished waves of this workgroup
   __shared__ int wg_last;          // this workgroup finished its tile last (fused tail)
   if (a.go && *a.go == 0) return;  // speculatively enqueued sweep that must not run
@@ -556,7 +557,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
       const int fh = ifloor16(hs), fw = ifloor16(ws);
       const float dh = fph - hs, dw = fpw - ws;
       float v;
-      if constexpr (TB) v = psf_tab<true>(tab, tinv, fmaf(dh, dh, dw * dw));
+      if constexpr (TB) v = psf_tab(tab, tinv, fmaf(dh, dh, dw * dw));
       else v = psf_raw<MODEL>(m, fmaf(dh, dh, dw * dw));
       if (lane < HW) pcw[s * HW + lane] = (abs(ph - fh) <= m.R && abs(pw - fw) <= m.R) ? v : 0.f;
     }
@@ -1235,7 +1236,9 @@ static bool tail_fusable(const smcdet_image_model_t& m, int N, int S, uint32_t f
 // ---- the radial PSF table (psf_tab, device.h) --------------------------------
 // Device copies live in a module-scope table of slots, one per (device, PSF
 // parameters); a slot is filled once (upload + stream synchronisation, so any
-// later launch on any stream sees it) and reused by every later sweep.
+// later launch on any stream sees it), reused by every later sweep of those
+// parameters and never recycled (parameter sets past kTabSlots fall back to
+// the exp2/log2 form).
 namespace smcdet {
 constexpr int kTabSlots = 8;
 __device__ float4 g_psf_tab[kTabSlots][kTabNodes];
@@ -1320,10 +1323,8 @@ static int psf_table_device(const smcdet_image_model_t& mdl, const DevModel& m, 
   void* base = nullptr;
   if (hipGetSymbolAddress(&base, HIP_SYMBOL(g_psf_tab)) != hipSuccess)
     return set_error(SMCDET_EHIP, "hipGetSymbolAddress(g_psf_tab) failed");
-  int used = 0;
   for (const TabEntry& e : g_tab_entries) {
     if (e.dev != dev) continue;
-    ++used;
     if (memcmp(e.key, key, sizeof(key)) == 0) {
       if (e.slot < 0) return SMCDET_OK;  // known not to meet the accuracy bound
       *out = reinterpret_cast<const float4*>(base) + (size_t)e.slot * kTabNodes;
@@ -1343,16 +1344,17 @@ static int psf_table_device(const smcdet_image_model_t& mdl, const DevModel& m, 
   int slots = 0;
   for (const TabEntry& x : g_tab_entries) slots += (x.dev == dev && x.slot >= 0);
   if (slots >= kTabSlots) {
-    // every slot taken: wait for the device, then start over with this one
-    if (hipDeviceSynchronize() != hipSuccess) return set_error(SMCDET_EHIP, "sync failed");
-    std::vector<TabEntry> keep;
-    for (const TabEntry& x : g_tab_entries)
-      if (x.dev != dev) keep.push_back(x);
-    g_tab_entries.swap(keep);
-    slots = 0;
+    // every slot taken (more than kTabSlots PSF parameter sets on this
+    // device): this model keeps the exp2/log2 form.  A slot is never reused,
+    // so a pointer handed out earlier stays valid for any later launch.
+    e.slot = -1;
+    g_tab_entries.push_back(e);
+    return SMCDET_OK;
   }
-  (void)used;
   e.slot = slots;
+  // the one synchronisation: the first sweep of a PSF parameter set uploads
+  // its table and waits for it (so the table's first use cannot sit inside a
+  // stream capture; later launches only read the slot)
   if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_psf_tab), host.data(), kTabNodes * sizeof(float4),
                              (size_t)e.slot * kTabNodes * sizeof(float4), hipMemcpyHostToDevice,
                              st) != hipSuccess ||

@@ -564,8 +564,12 @@ __device__ __forceinline__ void tile_work(const TileArgs& a, int t, float* buf, 
       ssum[h] = tree_sum(s);
       qsum[h] = tree_sum(q);
     }
-    // one reduction for the sum and the sum of squares: ESS = 1 / sum W^2
-    // = (sum e)^2 / sum e^2 (sampler.py:187-190), in double
+    // one reduction for the sum and the sum of squares: ESS = (sum e)^2 /
+    // sum e^2 in double -- algebraically the reference's 1 / sum W^2
+    // (sampler.py:189), which squares and sums the float32-rounded weights
+    // W = softmax in float32; the two agree to float32 rounding (relative
+    // ~1e-7), not bit for bit (a second reduction over W after sum e is known
+    // would cost one more block barrier per tile pass)
     SMC_TRACE(trow, 7);
     double se, qe;
     vblock_sum2d<NT>(ssum, qsum, se, qe, &red, parity);

@@ -205,8 +205,9 @@ def test_c5_statistical_vs_oracle():
     to float precision).  256 GPU runs of the cutout in one sampler."""
     ref = _load("stats_c5_oracle.json")
     rr = ref["runs"]
-    if len(rr) < 48:
-        pytest.skip(f"stats_c5_oracle.json: {len(rr)} oracle runs (< 48)")
+    need = int(os.environ.get("SMCDET_C5_MIN_RUNS", "48"))  # (lower: a trial run)
+    if len(rr) < need:
+        pytest.skip(f"stats_c5_oracle.json: {len(rr)} oracle runs (< {need})")
     cfg = ref["config"]
     assert (cfg["N"], cfg["K"], cfg["smax"]) == (8192, 100, 6)
     img = torch.tensor(ref["image"], dtype=torch.float32, device=DEV)

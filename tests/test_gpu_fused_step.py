@@ -136,14 +136,19 @@ def test_launch_timing_on_dispatch_events():
     _assert_same(ta, _steps(b, 3))
 
 
-@pytest.mark.parametrize("stopping,N", [("lockstep", 1024), ("independent", 1024),
-                                        ("lockstep", 1000)])
-def test_ancestor_bins_equal_indices(stopping, N):
+@pytest.mark.parametrize("stopping,N,fused", [("lockstep", 1024, False),
+                                              ("independent", 1024, False),
+                                              ("lockstep", 1000, False),
+                                              ("lockstep", 1001, False),
+                                              ("independent", 1024, True)])
+def test_ancestor_bins_equal_indices(stopping, N, fused):
     """The step's tile pass hands the next systematic resampling to the next
     sweep as bins + offset (AncestorBins, ABI 16), whose waves search their
     own ancestors: the same indices and the same run, bit for bit, as the
     int64 index hand-over (SMCsampler.ancestor_bins = False); N = 1000: the
-    search's division form for N not a power of two."""
+    search's division form for N not a power of two; N = 1001: bins_out + t*N
+    not 16-byte aligned (the tile pass's scalar store path, ADVICE r4);
+    fused: the bins written by the sweep's in-kernel tail (one launch)."""
     from smcdet_amd.sampler import SMCsampler
     out = []
     for bins in (True, False):
@@ -154,6 +159,7 @@ def test_ancestor_bins_equal_indices(stopping, N):
                        M71["flux_detection_threshold"], 200, print_every=10 ** 9, seed=21,
                        device=DEV, stopping=stopping)
         s.ancestor_bins = bins
+        s.fused_step = fused
         s.run()
         torch.cuda.synchronize()
         out.append({k: getattr(s, k).detach().cpu().numpy().copy()

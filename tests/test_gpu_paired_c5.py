@@ -37,7 +37,7 @@ from tests._params import GOLDEN, M71, p_m71_mh, p_m71_model, p_m71_prior
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 TARGET = "stats_c5_oracle.json"
-MIN_RUNS = 48
+MIN_RUNS = int(os.environ.get("SMCDET_C5_MIN_RUNS", "48"))  # (lower: a trial run)
 CHUNKS = 8
 _results = {}
 
