@@ -166,6 +166,11 @@ def parse():
     ap.add_argument("--no-spread", action="store_true")
     # skip the C4 / C5 / C3-rank-share legs of the default C2 run
     ap.add_argument("--no-legs", action="store_true")
+    # seconds of back-to-back untimed steps before the warmup steps (then the
+    # sampler restarts from a fresh initialisation): the chip's clock ramps
+    # up over its first ~60 busy steps after idle, which the W = 5 warmup
+    # steps do not cover (scripts/warmup_probe.py); 0 = off
+    ap.add_argument("--prewarm-s", type=float, default=2.0)
     # diagnostic MH flags (A/B timing: e.g. 2048 = SMCDET_MH_NO_PSF_CACHE)
     ap.add_argument("--mh-debug-flags", type=int, default=0)
     # CPU rehearsal of the multi-rank bookkeeping (gloo, RehearsalSampler: no
@@ -907,6 +912,26 @@ def main():
         idx, s._pending_idx = s._pending_idx, None
         s._step(idx)
 
+    prewarm = None
+    if args.prewarm_s > 0 and not REHEARSAL:
+        # the clock's ramp from idle, outside the measured run: untimed steps
+        # until prewarm_s seconds have passed, then a fresh start of the same
+        # sampler (initialise, first temper), so the timed steps are SMC
+        # iterations W+1..W+K of a new run, as without the prewarm
+        t_pw, n_pw = time.perf_counter(), 0
+        while time.perf_counter() - t_pw < args.prewarm_s:
+            for _ in range(10):
+                step()
+            n_pw += 10
+            _sync()
+        s.initialize()
+        s._temper_reweight(with_resample=True)
+        prewarm = {"seconds": round(time.perf_counter() - t_pw, 3), "steps": n_pw,
+                   "note": "untimed back-to-back steps before the warmup steps (the chip's "
+                           "clock ramps up over its first ~60 busy steps after idle: C2 sweep "
+                           "0.273 -> 0.246 ms, scripts/warmup_probe.py), then the sampler "
+                           "restarts from initialize(); the timed steps are iterations "
+                           "W+1..W+K of that fresh run"}
     for _ in range(args.warmup):
         step()
     _sync()
@@ -1003,6 +1028,7 @@ def main():
         "data": "synthetic (M71 prior + image model, seed 1000+rank)",
         "config": dict(cfg, mode="full" if args.full_recompute else "incremental",
                        parallelism=f"tile-sharded x{world}"),
+        "prewarm": prewarm,
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": f"smcdet {args.kernel}_sweep_kernel", "kernel_ms": mh_ms,

@@ -20,6 +20,9 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--sweep", default="mh_sweep_kernel")
 ap.add_argument("--tile", default="tile_kernel")
 ap.add_argument("--json", default=None)
+# the last N clean steps instead of --skip/--steps (a trace whose timed
+# region is its end, e.g. bench.py with the prewarm and no untimed tail)
+ap.add_argument("--tail", type=int, default=0)
 a = ap.parse_args()
 
 rows = [r for r in csv.DictReader(open(a.trace))]
@@ -38,7 +41,7 @@ for n, i in enumerate(sweeps[:-1]):
     steps.append(dict(sweep_us=(e0 - s0) / 1e3, gap_sweep_tile_us=(s1 - e0) / 1e3,
                       tile_us=(e1 - s1) / 1e3, gap_tile_sweep_us=(ev[j][1] - e1) / 1e3,
                       step_us=(ev[j][1] - s0) / 1e3))
-sel = steps[a.skip:a.skip + a.steps]
+sel = steps[-a.tail:] if a.tail > 0 else steps[a.skip:a.skip + a.steps]
 out = {"steps": len(sel), "source": a.trace}
 for k in sel[0]:
     v = np.array([s[k] for s in sel])
