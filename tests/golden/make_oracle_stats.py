@@ -34,6 +34,7 @@ tests/test_oracle_cached.py) and two more targets exist:
     python tests/golden/make_oracle_stats.py c2_moderate_4096_k100 <n_runs> [first_seed] [threads] [f64|f32]
     python tests/golden/make_oracle_stats.py c5 <n_runs> [first_seed] [threads]
     python tests/golden/make_oracle_stats.py queue <cycles> [threads]   # round-robin of all three
+    python tests/golden/make_oracle_stats.py merge <dir>/stats_*.json    # fold in another dir's runs
 """
 import json
 import os
@@ -144,11 +145,16 @@ ORACLE_DESC = {
            "re-render) + oracle/smc_oracle.py in float32 (temper objective, reweighting)"}
 
 
+# where the targets are written (SMCDET_ORACLE_OUT: e.g. gpurun_out/ on a GPU
+# box, whose host cores run a batch of seeds; `merge` folds them in here)
+OUT = os.environ.get("SMCDET_ORACLE_OUT", HERE)
+
+
 def one_c2(which, seed, threads, arith):
     ref = json.load(open(os.path.join(HERE, f"stats_{which}.json")))
     cfg = dict(ref["config"])
     suffix = "_oracle" if arith == "f64" else "_oracle_f32"
-    out_path = os.path.join(HERE, f"stats_{which}{suffix}.json")
+    out_path = os.path.join(OUT, f"stats_{which}{suffix}.json")
     if seed in _done(out_path):
         return
     t0 = time.perf_counter()
@@ -163,7 +169,7 @@ def one_c2(which, seed, threads, arith):
 
 def one_c5(seed, threads, arith="f64"):
     ref = json.load(open(os.path.join(HERE, "stats_c5.json")))
-    out_path = os.path.join(HERE, "stats_c5_oracle.json" if arith == "f64"
+    out_path = os.path.join(OUT, "stats_c5_oracle.json" if arith == "f64"
                             else "stats_c5_oracle_f32.json")
     if seed in _done(out_path):
         return
@@ -180,6 +186,16 @@ def one_c5(seed, threads, arith="f64"):
 
 def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "c2_moderate_4096_k100"
+    if which == "merge":
+        # merge <file> ...: runs of another directory's targets into the ones here
+        for src in sys.argv[2:]:
+            doc = json.load(open(src))
+            dst = os.path.join(HERE, os.path.basename(src))
+            for r in doc["runs"]:
+                _append(dst, doc["config"], doc["image"], r)
+            print("merged", len(doc["runs"]), "runs of", src, "->", dst,
+                  len(json.load(open(dst))["runs"]), "runs")
+        return
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 32
     if which == "queue":
         # round-robin: C5 (f64), C2 f64 (seeds 48..), C2 f32 (seeds 0..)
