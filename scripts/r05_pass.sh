@@ -17,7 +17,7 @@ SQSET="SQ_INSTS_VALU SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP32_TRANS SQ_
 SQ2SET="SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"
 SQ3SET="SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SCRATCH SQ_WAVES"
 if has tests; then
-  SMCDET_PAIRED_OUT=$D/paired.json SMCDET_PAIRED_C5_OUT=$D/paired_c5.json \
+  SMCDET_PAIRED_OUT=$D/paired.json SMCDET_PAIRED_C5_OUT=$D/paired_c5.json SMCDET_C5_STATS_OUT=$D/c5_stats.json \
     timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest ${TESTS:-tests -m gpu} -v \
     -p no:cacheprovider --timeout 300 --timeout-method thread > $D/pytest.log 2>&1
   step tests $?
