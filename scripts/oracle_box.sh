@@ -7,15 +7,18 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 D=gpurun_out/oracle_box${TAG:-}
 mkdir -p $D
-export SMCDET_ORACLE_OUT=$D OMP_WAIT_POLICY=passive
+export OMP_WAIT_POLICY=passive
+mkdir -p $D/a $D/b   # one output directory per process (no read-modify-write race)
 FIRST=${FIRST:-1000}; N=${N:-200}; LIMIT=${LIMIT:-1080}
 W=${WHAT:-c2_moderate_4096_k100}
-timeout -k 10 $LIMIT python -u tests/golden/make_oracle_stats.py $W $N $FIRST 8 f64 > $D/f64.log 2>&1 &
+SMCDET_ORACLE_OUT=$D/a timeout -k 10 $LIMIT python -u tests/golden/make_oracle_stats.py $W $N $FIRST 8 f64 > $D/f64.log 2>&1 &
 p1=$!
 if [ "$W" = "c5" ]; then
-  timeout -k 10 $LIMIT python -u tests/golden/make_oracle_stats.py c5 $N $((FIRST + 500)) 8 f64 > $D/f64b.log 2>&1 &
+  SMCDET_ORACLE_OUT=$D/b timeout -k 10 $LIMIT python -u tests/golden/make_oracle_stats.py c5 $N $((FIRST + 500)) 8 f64 > $D/f64b.log 2>&1 &
+elif [ -n "${F64B:-}" ]; then
+  SMCDET_ORACLE_OUT=$D/b timeout -k 10 $LIMIT python -u tests/golden/make_oracle_stats.py $W $N $((FIRST + N)) 8 f64 > $D/f64b.log 2>&1 &
 else
-  timeout -k 10 $LIMIT python -u tests/golden/make_oracle_stats.py $W $N $FIRST 8 f32 > $D/f32.log 2>&1 &
+  SMCDET_ORACLE_OUT=$D/b timeout -k 10 $LIMIT python -u tests/golden/make_oracle_stats.py $W $N $FIRST 8 f32 > $D/f32.log 2>&1 &
 fi
 p2=$!
 # progress for the harness's hang detector
