@@ -9,8 +9,10 @@ the reference's runs allow (3 pooled SE; the 1% gates of north_star are the
 GPU tests' against the larger oracle targets):
 
   * C5 (stats_c5_oracle.json vs stats_c5.json, 8 reference CS-SMC runs):
-    per-count log Z for s = 1..6, p(s|x), and log Z_0 (the empty catalog,
-    float64 vs the reference's float32 -- relative 1e-6);
+    per-count log Z for s = 1..6 (3 pooled SE), the winning count of each
+    reference run against the oracle's win shares (exact binomial tests), and
+    log Z_0 (the empty catalog, float64 vs the reference's float32 --
+    relative 1e-6);
   * C2 (stats_c2_moderate_4096_k100_oracle[_f32].json vs the reference's K=100
     runs): mean log Z, SMC iterations; the float64 and float32-class oracle
     runs of the same seeds against each other.
@@ -49,10 +51,18 @@ def test_c5_oracle_target_vs_reference_runs():
     for s in range(1, 7):
         d = ol[:, s].mean() - rl[:, s].mean()
         assert abs(d) <= 3 * _se(ol[:, s], rl[:, s]), (s, ol[:, s].mean(), rl[:, s].mean())
-    rp = np.array([r["count_posterior"] for r in ref["runs"]])
-    op = np.array([r["count_posterior"] for r in orc["runs"]])
-    se = np.sqrt(rp.var(0, ddof=1) / len(rp) + op.var(0, ddof=1) / len(op))
-    assert np.all(np.abs(op.mean(0) - rp.mean(0)) <= 3 * se + 1e-6), (op.mean(0), rp.mean(0))
+    # p(s|x): a run's posterior is nearly one-hot (the count whose evidence
+    # wins), so 8 reference runs are 8 draws of the winning count; each
+    # count's reference wins against the oracle's win share by an exact
+    # two-sided binomial test (an SE from 8 near-0/1 values, all 0 for a
+    # count that won no reference run, is no error estimate)
+    from scipy.stats import binomtest
+    rw = np.array([np.argmax(r["count_posterior"]) for r in ref["runs"]])
+    ow = np.array([np.argmax(r["count_posterior"]) for r in orc["runs"]])
+    for s in range(7):
+        p_o = min(max((ow == s).mean(), 0.5 / len(ow)), 1 - 0.5 / len(ow))
+        k = int((rw == s).sum())
+        assert binomtest(k, len(rw), p_o).pvalue > 0.01, (s, k, len(rw), p_o)
     # every stratum ran to temperature 1 within the iteration cap
     for r in orc["runs"]:
         assert all(t[-1] == 1.0 for t in r["tau_trace"][1:]), r["seed"]
