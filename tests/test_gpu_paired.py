@@ -18,18 +18,28 @@ first iterations and leave each other at iteration 3-12
 variant, the reference's own float32 full re-render and a GPU run tempered
 by the oracle's float64 tile pass included.  From there on a twin is a new
 draw of the run's random outcome, so on "fragile" seeds (oracle log Z
-between the modes) the mode is not a function of the draws.  The test
-therefore checks:
+between the modes) the mode is not a function of the draws.
+
+The gates come from the round-5 evidence (profiles/r05/paired_c2_all.json:
+all 257 oracle runs replayed): the GPU and the oracle end in different modes
+in 14 of 257 pairs (5.4%; 8 GPU-lower-only, 6 oracle-lower-only, McNemar
+p = 0.79), the GPU and its own reference-arithmetic twin in 12 (4.7%), and
+the float32-class oracle and the float64 oracle in 15 of 191
+(scripts/mode_share.py) -- a discordance rate of ~5% is the chaos of
+near-tie decisions, whatever the two arithmetics.  The test checks:
   * the pairing: ladders equal (|delta tau| <= 1e-5) for the first two
     iterations in >= 90% of runs;
-  * agreement where runs are robust: the same mode (cut: median - 40 nats; the
-    lower mode sits ~65-80 nats below) in >= 40 of 48 runs, and median
-    |delta log Z| <= 5 nats over the runs in the same mode;
+  * agreement where runs are robust: the number of pairs in different modes
+    (cut: median - 40 nats; the lower mode sits ~65-80 nats below) is
+    consistent with that 5.4% rate (one-sided binomial p > 0.001: at most 9
+    of the default 48), and median |delta log Z| <= 5 nats over the runs in
+    the same mode;
   * no systematic excess: McNemar's exact test on the runs in different
     modes (GPU lower only vs oracle lower only), two-sided p > 0.01.
 The reference-arithmetic twin (SingleComponentMH(full_recompute=True)) is
 recorded next to it as a control (SMCDET_PAIRED_OUT summary).
 """
+DISCORDANCE = 14 / 257  # profiles/r05/paired_c2_all.json
 import json
 import os
 
@@ -163,7 +173,9 @@ def test_paired_runs_same_mode():
         with open(path, "w") as f:
             json.dump(summary, f, indent=1)
     print({k: v for k, v in summary.items() if k != "runs"})
+    from scipy.stats import binomtest
     assert (first >= 2).mean() >= 0.9, summary["ladder_first_divergence"]
-    assert gpu["same_mode"] >= len(res) - 8, gpu
+    discordant = len(res) - gpu["same_mode"]
+    assert binomtest(discordant, len(res), DISCORDANCE, alternative="greater").pvalue > 0.001, gpu
     assert gpu["abs_dlogz_median_same_mode"] <= 5.0, gpu
     assert gpu["mcnemar_p"] > 0.01, gpu
