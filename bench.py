@@ -913,7 +913,21 @@ def main():
         s._step(idx)
 
     prewarm = None
+    cold = None
     if args.prewarm_s > 0 and not REHEARSAL:
+        # for the record: the same W + K steps timed from a cold chip first
+        # (what the line measured before round 5), then the prewarm
+        for _ in range(args.warmup):
+            step()
+        _sync()
+        t_c = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        _sync()
+        cold_ms = (time.perf_counter() - t_c) / args.steps * 1e3
+        cold = {"ms_per_step": cold_ms, "value": world * steps_per_step / (cold_ms * 1e-3),
+                "note": "the same W warmup + K timed steps before the prewarm (this rank; "
+                        "the chip's clock still ramping from idle)"}
         # the clock's ramp from idle, outside the measured run: untimed steps
         # until prewarm_s seconds have passed, then a fresh start of the same
         # sampler (initialise, first temper), so the timed steps are SMC
@@ -931,7 +945,7 @@ def main():
                            "clock ramps up over its first ~60 busy steps after idle: C2 sweep "
                            "0.273 -> 0.246 ms, scripts/warmup_probe.py), then the sampler "
                            "restarts from initialize(); the timed steps are iterations "
-                           "W+1..W+K of that fresh run"}
+                           "W+1..W+K of that fresh run", "cold": cold}
     for _ in range(args.warmup):
         step()
     _sync()
