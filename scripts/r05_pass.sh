@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 GPU pass.  STEPS selects: tests bench profile c4pmc c5pmc postbench
+# Round-5 GPU pass.  STEPS selects: tests smoke bench profile c4pmc c5pmc postbench
 # Each GPU step has its own limit; a crash, abort or timeout ends the script
 # (test failures, rc 1, do not).
 set -u
@@ -22,6 +22,11 @@ if has tests; then
     -p no:cacheprovider --timeout 300 --timeout-method thread > $D/pytest.log 2>&1
   step tests $?
   grep -E "^FAILED|passed|failed" $D/pytest.log | tail -12
+fi
+if has smoke; then
+  timeout -k 10 240 python __graft_entry__.py smoke > $D/smoke.log 2>&1
+  step smoke $?
+  tail -2 $D/smoke.log
 fi
 if has bench; then
   timeout -k 10 400 python bench.py > $D/bench.log 2>&1
