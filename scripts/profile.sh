@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/prof}
 KRE=${KRE:-mh_sweep}  # kernel-name regex of the PMC passes
 mkdir -p $OUT
-B="bench.py --steps ${PSTEPS:-20} --warmup 3 --no-cpu-baseline --no-full-run --no-vs-ref --no-c3 --no-legs --no-spread ${BENCH_ARGS:-}"
+B="bench.py --steps ${PSTEPS:-20} --warmup 3 --no-cpu-baseline --no-full-run --no-vs-ref --no-c3 --no-legs --no-spread --prewarm-s 0 ${BENCH_ARGS:-}"
 run() {  # $1 = name, rest = rocprofv3 args
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" -T -f csv -d $OUT/$name -o run -- python3 $B > $OUT/$name.log 2>&1

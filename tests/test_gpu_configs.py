@@ -157,6 +157,49 @@ def test_c4_statistical_vs_reference():
         hist.mean(0).round(3), h_ref.mean(0).round(3))
 
 
+def test_c4_statistical_vs_oracle():
+    """C4 against the oracle's target (tests/golden/stats_c4_oracle.json,
+    make_oracle_stats.py: complete runs of the float64 restatement of the
+    reference's SMCsampler on the stats_c4.json cutout, 8x8, S = 10,
+    N = 4096, K = 100): mean log Z within 3 pooled SE and 1%, final ESS,
+    SMC iterations and mean total flux within 3 pooled SE, and the pruned
+    count histogram within total variation 0.05 (SURVEY.md §8d's parity
+    metric).  128 GPU runs of the cutout in one batch."""
+    ref = _load("stats_c4_oracle.json")
+    rr = ref["runs"]
+    if len(rr) < 48:
+        pytest.skip(f"stats_c4_oracle.json: {len(rr)} oracle runs (< 48)")
+    cfg = ref["config"]
+    assert (cfg["tile"], cfg["N"], cfg["S"], cfg["K"]) == (8, 4096, 10, 100)
+    img = torch.tensor(ref["image"], dtype=torch.float32, device=DEV)
+    n = 128
+    b = _c4_batch(img[None].expand(n, H, H).contiguous(), 778)
+    b.run()
+    r = b.results()
+    lz = r["log_normalizing_constant"].cpu().double().numpy()
+    fe = r["ess"].cpu().double().numpy()
+    it = r["num_iters"].cpu().double().numpy()
+    fl = r["fluxes"].sum(-1).mean(-1).cpu().double().numpy()
+    lz_o = np.array([x["logZ"] for x in rr])
+    fe_o = np.array([x["final_ess"] for x in rr])
+    it_o = np.array([x["iters"] for x in rr], np.float64)
+    fl_o = np.array([x["mean_total_flux"] for x in rr])
+    pc = r["pruned_counts"].cpu().numpy()
+    hist = np.stack([np.bincount(p, minlength=11)[:11] / p.size for p in pc]).mean(0)
+    h_o = np.array([x["pruned_hist"] for x in rr])[:, :11].mean(0)
+    tv = 0.5 * np.abs(hist - h_o).sum()
+    print(f"C4 vs oracle ({len(rr)} runs): log Z {lz.mean():.2f} vs {lz_o.mean():.2f} "
+          f"(pooled SE {_se(lz, lz_o):.2f}); final ESS {fe.mean():.1f} vs {fe_o.mean():.1f}; "
+          f"iters {it.mean():.2f} vs {it_o.mean():.2f}; total flux {fl.mean():.2f} vs "
+          f"{fl_o.mean():.2f}; pruned-count TV {tv:.4f}")
+    assert abs(lz.mean() - lz_o.mean()) <= 3 * _se(lz, lz_o), (lz.mean(), lz_o.mean())
+    assert abs(lz.mean() - lz_o.mean()) <= 0.01 * abs(lz_o.mean()), (lz.mean(), lz_o.mean())
+    assert abs(fe.mean() - fe_o.mean()) <= 3 * _se(fe, fe_o), (fe.mean(), fe_o.mean())
+    assert abs(it.mean() - it_o.mean()) <= max(3 * _se(it, it_o), 0.5), (it.mean(), it_o.mean())
+    assert abs(fl.mean() - fl_o.mean()) <= 3 * _se(fl, fl_o), (fl.mean(), fl_o.mean())
+    assert tv <= 0.05, (hist.round(3), h_o.round(3))
+
+
 def _c5(images, seed, N=8192):
     from smcdet_amd.cssmc import CountStratifiedSMC
     return CountStratifiedSMC(images.reshape(1, -1, H, H), H, p_m71_prior(H, 0, 6),
