@@ -101,3 +101,21 @@ def test_c2_f32_and_f64_oracle_runs_of_the_same_seeds():
     assert np.median(first) >= 2, first
     d = np.array([f32[s]["logZ"] - f64[s]["logZ"] for s in common])
     assert abs(d.mean()) <= 3 * d.std(ddof=1) / np.sqrt(d.size) + 1e-9, (d.mean(), d.std())
+
+
+def test_c4_oracle_target_vs_reference_runs():
+    """C4 (stats_c4_oracle.json, float64 restatement runs of the reference's
+    SMCsampler on the "m71" 8x8 cutout, S = 10, N = 4096, K = 100) against the
+    reference's own 20 runs (stats_c4.json): mean log Z, final ESS, SMC
+    iterations within 3 pooled SE; pruned-count histograms within total
+    variation 0.05."""
+    ref = _load("stats_c4.json", 20)
+    orc = _load("stats_c4_oracle.json", 48)
+    assert orc["image"] == ref["image"]
+    for key in ("logZ", "final_ess", "iters"):
+        a = np.array([r[key] for r in orc["runs"]], float)
+        b = np.array([r[key] for r in ref["runs"]], float)
+        assert abs(a.mean() - b.mean()) <= max(3 * _se(a, b), 1e-9), (key, a.mean(), b.mean())
+    ha = np.array([r["pruned_hist"] for r in orc["runs"]])[:, :11].mean(0)
+    hb = np.array([r["pruned_hist"] for r in ref["runs"]])[:, :11].mean(0)
+    assert 0.5 * np.abs(ha - hb).sum() <= 0.05, (ha.round(3), hb.round(3))
