@@ -71,12 +71,24 @@ def test_c5_oracle_target_vs_reference_runs():
 @pytest.mark.parametrize("target", ["stats_c2_moderate_4096_k100_oracle.json",
                                     "stats_c2_moderate_4096_k100_oracle_f32.json"])
 def test_c2_oracle_target_vs_reference_runs(target):
+    """The reference's few K = 100 runs (~75 min each) against the oracle's
+    hundreds: log Z is bimodal (a lower mode ~65-80 nats down holds ~13% of
+    the oracle's runs), so a mean +- SE from a dozen reference runs -- which
+    may hold none of the lower mode -- is no error estimate; the law is
+    compared instead: medians within 1%, a two-sample rank test, and the
+    reference's count of lower-mode runs against the oracle's share (exact
+    binomial)."""
+    from scipy.stats import binomtest, mannwhitneyu
     ref = _load("stats_c2_moderate_4096_k100.json", 8)
     orc = _load(target, 8)
     assert orc["image"] == ref["image"]
     rl = np.array([r["logZ"] for r in ref["runs"]])
     ol = np.array([r["logZ"] for r in orc["runs"]])
-    assert abs(ol.mean() - rl.mean()) <= 3 * _se(ol, rl), (ol.mean(), rl.mean())
+    assert abs(np.median(ol) - np.median(rl)) <= 0.01 * abs(np.median(rl))
+    assert mannwhitneyu(ol, rl).pvalue > 0.001, (np.median(ol), np.median(rl))
+    cut = -4310.0
+    p_o = (ol < cut).mean()
+    assert binomtest(int((rl < cut).sum()), len(rl), p_o).pvalue > 0.01, (p_o, (rl < cut).sum())
     ri = np.array([r["iters"] for r in ref["runs"]], float)
     oi = np.array([r["iters"] for r in orc["runs"]], float)
     assert abs(oi.mean() - ri.mean()) <= max(3 * _se(oi, ri), 0.5), (oi.mean(), ri.mean())
@@ -107,8 +119,7 @@ def test_c4_oracle_target_vs_reference_runs():
     """C4 (stats_c4_oracle.json, float64 restatement runs of the reference's
     SMCsampler on the "m71" 8x8 cutout, S = 10, N = 4096, K = 100) against the
     reference's own 20 runs (stats_c4.json): mean log Z, final ESS, SMC
-    iterations within 3 pooled SE; pruned-count histograms within total
-    variation 0.05."""
+    iterations and every pruned-count histogram bin within 3 pooled SE."""
     ref = _load("stats_c4.json", 20)
     orc = _load("stats_c4_oracle.json", 48)
     assert orc["image"] == ref["image"]
@@ -116,6 +127,12 @@ def test_c4_oracle_target_vs_reference_runs():
         a = np.array([r[key] for r in orc["runs"]], float)
         b = np.array([r[key] for r in ref["runs"]], float)
         assert abs(a.mean() - b.mean()) <= max(3 * _se(a, b), 1e-9), (key, a.mean(), b.mean())
-    ha = np.array([r["pruned_hist"] for r in orc["runs"]])[:, :11].mean(0)
-    hb = np.array([r["pruned_hist"] for r in ref["runs"]])[:, :11].mean(0)
-    assert 0.5 * np.abs(ha - hb).sum() <= 0.05, (ha.round(3), hb.round(3))
+    # the pruned-count histogram bin by bin (3 pooled SE; 20 reference runs do
+    # not resolve SURVEY §8d's total variation 0.05 -- that gate is the GPU
+    # test's against this target's 400 runs)
+    ha = np.array([r["pruned_hist"] for r in orc["runs"]])[:, :11]
+    hb = np.array([r["pruned_hist"] for r in ref["runs"]])[:, :11]
+    se = np.sqrt(ha.var(0, ddof=1) / len(ha) + hb.var(0, ddof=1) / len(hb))
+    # (a 1e-3 floor: bins that hold below 0.1% of the posterior in both,
+    # where one run's stray catalog is the whole signal)
+    assert np.all(np.abs(ha.mean(0) - hb.mean(0)) <= 3 * se + 1e-3), (ha.mean(0), hb.mean(0))
