@@ -584,6 +584,11 @@ def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
             out["executed"]["issue_cycles_per_particle_step"] = cyc
             out["executed"]["issue_cycles_available"] = avail
             out["executed"]["issue_cycle_frac"] = cyc / avail
+            # the model-free figure: SIMD cycles the launch had per VALU
+            # wave-instruction it issued (one stream alone needs 4.2 for a
+            # plain op, 8.6 for a transcendental; many waves interleave below
+            # that -- near 4 the SIMDs issue VALU every slot they have)
+            out["executed"]["simd_cycles_per_valu_inst"] = avail / per_step["SQ_INSTS_VALU"]
             # the same at the clock the launch actually ran at: GRBM_GUI_ACTIVE
             # / 8 XCDs / the profiled launch's duration (MI355X_MICROARCH.md,
             # "DVFS give-back"); the profiled pass's own cycles per particle-step
