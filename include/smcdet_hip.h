@@ -97,6 +97,11 @@ extern "C" {
  * by float32 rounding of the profile, ~3e-7 relative).  Measured slower at
  * 32x32 (its LDS reads) and even at 8x8, so off by default */
 #define SMCDET_MH_PSF_TABLE 8192u
+/* diagnostic: M71 tiles of 16x16 .. 1024 pixels without the block form of
+ * same-anchor steps (the union window's first 16 rows and columns as one
+ * 16x16 block whose Gaussian PSF terms come from a rank-4 MFMA); results
+ * differ by float32 rounding of the profile */
+#define SMCDET_MH_NO_BLOCK 16384u
 
 /* Image model (smcdet/images.py:6-26 ImageModel, :105-145 M71ImageModel). */
 typedef struct smcdet_image_model {

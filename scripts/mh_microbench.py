@@ -30,6 +30,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--full", action="store_true", help="include the full-recompute variant")
     ap.add_argument("--only", default=None, help="run just this variant (for rocprofv3 --pmc)")
+    ap.add_argument("--variants", default=None,
+                    help="comma-separated subset of the variants, interleaved (A/B)")
+    ap.add_argument("--no-extra", action="store_true", help="skip the tile/loglik kernel timings")
+    ap.add_argument("--block-slots", default=None,
+                    help="comma-separated SMCDET_MH_BLOCK_SLOTS values, one variant each")
     ap.add_argument("--tau", type=float, default=0.3)
     # library-independent inputs (torch CPU generator + the c2_moderate fixture
     # image), so that libraries whose prior/noise kernels draw different
@@ -82,13 +87,22 @@ def main():
                     _hip, "SMCDET_MH_ABLATE_LIKELIHOOD") else 256),
                 "no_proposal": (False, 512),
                 "no_both": (False, 768),
-                "scalar_slots": (False, 1024)}
+                "scalar_slots": (False, 1024),
+                "no_block": (False, 16384)}
     if a.full:
         variants["full_recompute"] = (True, 0)
     for kk in (0, 1, 25, 200):
         variants[f"K={kk}"] = (False, 0, kk)
     if a.only:
         variants = {a.only: variants[a.only]}
+    # block-form thresholds (SMCDET_MH_BLOCK_SLOTS, read at every launch):
+    # variant "blk<n>" = the default form with that threshold (0 = off)
+    envs = {}
+    for n in (a.block_slots.split(",") if a.block_slots else []):
+        variants[f"blk{n}"] = (False, 0)
+        envs[f"blk{n}"] = n
+    if a.variants:
+        variants = {k: variants[k] for k in a.variants.split(",")}
     times = {k: [] for k in variants}
     mhs = {}
     for k, v in variants.items():
@@ -136,6 +150,8 @@ def main():
         "resample_only": lambda: _hip.check(_hip.lib().smcdet_resample_index(
             _hip.ptr(W), T, Np, 1, 1, 0, None, _hip.ptr(idx), _hip.stream_of(ll)), "r"),
     }
+    if a.no_extra:
+        extra = {}
     rates = {}
     if a.persist:
         # rate images of (locs, fluxes); every timed sweep reads them (and
@@ -147,6 +163,10 @@ def main():
         rates = {"rate_in": r_in, "rate_out": r_out}
     for r in range(a.rounds + 1):
         for k, mh in mhs.items():
+            if k in envs:
+                os.environ["SMCDET_MH_BLOCK_SLOTS"] = envs[k]
+            else:
+                os.environ.pop("SMCDET_MH_BLOCK_SLOTS", None)
             v = timeit(lambda: mh.run(img, counts, locs, fluxes, tau, prior=prior,
                                       image_model=model, **rates))
             if r:

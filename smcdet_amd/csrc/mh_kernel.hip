@@ -68,6 +68,7 @@ struct MhArgs {
   int skip_done;                     // SMCDET_MH_SKIP_DONE
   int no_psf_cache;                  // SMCDET_MH_NO_PSF_CACHE (diagnostic)
   int no_rcp_cache;                  // SMCDET_MH_NO_RCP_CACHE (diagnostic)
+  int blk_slots;                     // block form (M71, same anchor) from this many slots; 0: off
   const float4* psf_tab;             // M71 radial PSF table [kTabNodes] (or null: exp2/log2)
   float tab_inv_h;                   // 1 / its node spacing in r^2
   const float* img;                  // [T,H,W]
@@ -259,6 +260,42 @@ __device__ __forceinline__ f2 position_delta2(const DevModel& m, const float* xs
   f2 lgx = {0.f, 0.f};
   if constexpr (MODEL == SMCDET_MODEL_POISSON) lgx = f2{lg[p[0]], lg[p[1]]};
   return pix_delta2<MODEL>(m, x, lgx, lo, dl);
+}
+
+// ---- the 16x16 block form of a same-anchor M71 step (mh_sweep_kernel `block`)
+// The moved source's old and new PSF windows share their anchor, so the
+// union is one (clipped) box of at most 17x17 pixels.  Its first 16 rows and
+// columns are evaluated as a 16x16 block of the tile in the layout of
+// v_mfma_f32_16x16x4_f32's result (lane l holds rows 4(l>>4) + r, r < 4, of
+// column l & 15), the 17th row / column (<= 33 pixels) as one union-window
+// slot.  In the block, the profile's two Gaussian terms are separable,
+//   g exp2(k r^2) = g exp2(k dy^2) exp2(k dx^2),
+// so the rate change's Gaussian part,
+//   sum_k A[i][k] B[k][j],  k = (new, k1), (new, k2), (old, k1), (old, k2),
+//   A = +-amp (x b) exp2(k dy_i^2),  B = exp2(k dx_j^2),
+// is ONE rank-4 MFMA (exact f32 fused multiply-adds), built from 2 exp2 per
+// lane instead of 4 per pixel; the pixels keep only the power-law term
+// (exp2 of log2, old and new) and the likelihood change.  Same quantity as
+// position_delta's, rounded differently (a few ulp of the profile).
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// the per-pixel log-likelihood change of position_delta2 from the rate change
+// dl (M71; RV: the old pixel's 1/v read from the cache, the new one returned)
+template <int MODEL, bool RV>
+__device__ __forceinline__ f2 delta_from_dl2(const DevModel& m, f2 x, f2 lo, f2 dl,
+                                             const float* rv, const int (&p)[2], f2& lnew,
+                                             f2& rnew) {
+  lnew = lo + dl;
+  if constexpr (RV) {
+    const f2 r0 = {rv[p[0]], rv[p[1]]};
+    const f2 v1 = fma2(lnew, m.eta, m.s0sq);
+    const f2 r1 = rcp2(v1);
+    rnew = r1;
+    const f2 d0 = x - lo, d1 = x - lnew;
+    const f2 t = fma2(d0 * d0, r0, -(d1 * d1) * r1);
+    return fma2(t, 0.5f, (-0.5f * kLn2) * log2_2(v1 * r0));
+  }
+  return pix_delta2<MODEL>(m, x, f2{0.f, 0.f}, lo, dl);
 }
 
 // Small tiles with the PSF cache (PC): the moved source's old PSF values come
@@ -909,6 +946,75 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
           wave_sync();
         }
       };
+      // The 16x16 block form of a same-anchor step (M71; delta_from_dl2): the
+      // block of the tile at (r0, c0) holds the union box's first 16 rows and
+      // columns, the strip (one slot, s_*[4]) its 17th row and / or column.
+      // Taken where the box has at least 16 rows and columns and the
+      // per-pixel form would need a.blk_slots (default 5) slots: a same-box
+      // microbench at the C2 state measured the MH launch 4.7-5.2% faster
+      // with it there, and 1.2% faster where 4-slot boxes (16x16, or masked
+      // blocks of clipped boxes) took it too.
+      constexpr bool kBlk = MODEL == SMCDET_MODEL_M71 && PPL > 1 && !GL && !TB && PAIRED;
+      bool blk = false;
+      if constexpr (kBlk)
+        blk = same && a.blk_slots > 0 && nslots >= a.blk_slots && r1 - r0 >= 15 && c1 - c0 >= 15;
+      auto block = [&]() -> float {
+        const int li = lane & 15, lk = lane >> 4;
+        // MFMA operands: lane l is A[l & 15][l >> 4] and B[l >> 4][l & 15]
+        const bool knew = lk < 2;
+        const float kk = (lk & 1) ? m.k2 : m.k1;
+        const float ak = (knew ? amp_n : -amp_o) * ((lk & 1) ? m.b : 1.0f);
+        const float dy = ((float)(r0 + li) + 0.5f) - (knew ? P.hn : P.h);
+        const float dx = ((float)(c0 + li) + 0.5f) - (knew ? P.wn : P.w);
+        const float av = ak * fast_exp2(kk * (dy * dy));
+        const float bv = fast_exp2(kk * (dx * dx));
+        const f4 g = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        // this lane's block pixels: rows prow0 + r (r < 4) of column pcol
+        const int prow0 = r0 + 4 * lk, pcol = c0 + li;
+        const float fpw = (float)pcol + 0.5f;
+        const float dwo = fpw - P.w, dwn = fpw - P.wn;
+        const f2 dwo2 = {dwo * dwo, dwo * dwo}, dwn2 = {dwn * dwn, dwn * dwn};
+        const float po = amp_o * m.p0, pn = amp_n * m.p0;
+        const int pb = prow0 * m.W + pcol;
+        const float fph0 = (float)prow0 + 0.5f;
+        f2 acc = {0.f, 0.f};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f2 fph = {fph0 + (float)(2 * h), fph0 + (float)(2 * h + 1)};
+          const f2 dho = fph - P.h, dhn = fph - P.hn;
+          const f2 e3o = exp2_2(m.kb * log2_2(fma2(fma2(dho, dho, dwo2), m.k3, 1.0f)));
+          const f2 e3n = exp2_2(m.kb * log2_2(fma2(fma2(dhn, dhn, dwn2), m.k3, 1.0f)));
+          const f2 dl = f2{g[2 * h], g[2 * h + 1]} + fma2(e3n, pn, -po * e3o);
+          const int p[2] = {pb + 2 * h * m.W, pb + (2 * h + 1) * m.W};
+          const f2 lo = {lam[p[0]], lam[p[1]]};
+          const f2 x = {xs[p[0]], xs[p[1]]};
+          f2 lnew, rnew;
+          acc += delta_from_dl2<MODEL, RV>(m, x, lo, dl, rv, p, lnew, rnew);
+          s_lam[2 * h] = lnew.x;
+          s_lam[2 * h + 1] = lnew.y;
+          s_pix[2 * h] = p[0];
+          s_pix[2 * h + 1] = p[1];
+          if constexpr (RV) {
+            s_rv[2 * h] = rnew.x;
+            s_rv[2 * h + 1] = rnew.y;
+          }
+        }
+        // the strip: the box's 17th row, then its 17th column over the
+        // block's rows, one pixel per lane (<= 33)
+        const int nb = r1 > r0 + 15 ? c1 - c0 + 1 : 0;
+        const int nr = c1 > c0 + 15 ? 16 : 0;
+        const bool valid = lane < nb + nr, bot = lane < nb;
+        const int ph = bot ? r0 + 16 : r0 + (lane - nb);
+        const int pw = bot ? c0 + lane : c0 + 16;
+        const int p = valid ? ph * m.W + pw : HW + lane;
+        float lnew, rnew;
+        const float e = position_delta<MODEL, false, false, RV, false>(
+            m, xs, lg, lam, rv, tab, tinv, p, 0, 0, ph, pw, P, amp_o, amp_n, 0, 0, 0, 0, lnew, rnew);
+        s_lam[4] = lnew;
+        s_pix[4] = p;
+        if constexpr (RV) s_rv[4] = rnew;
+        return (acc.x + acc.y) + (valid ? e : 0.f);
+      };
       if constexpr (NSL == 1) {
         // small tiles (latency-bound at 7 waves per SIMD): one reduction and
         // accept after the merge measured faster (C4 4.95 vs 5.12 ms)
@@ -916,6 +1022,11 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
         if (nslots == 1) dsum = same ? slots(I1{}, Same{}) : slots(I1{}, Win{});
         dll = wave_sum(dsum);
         accept = __builtin_amdgcn_readfirstlane((fmaf(tau, dll, P.hast) >= log_u) ? 1 : 0);
+      } else if (blk) {
+        if constexpr (kBlk) {
+          nslots = 5;  // (finish: the writes of s_*[0..5): 4 block pixels + the strip)
+          finish(block(), I5{});
+        }
       } else if (nslots == 0) {
         finish(0.f, I0{});
       } else if (PAIRED && nslots == 1) {
@@ -1523,6 +1634,10 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
   a.skip_done = (flags & SMCDET_MH_SKIP_DONE) != 0;
   a.no_psf_cache = (flags & SMCDET_MH_NO_PSF_CACHE) != 0;
   a.no_rcp_cache = (flags & SMCDET_MH_NO_RCP_CACHE) != 0;
+  // the block form for same-anchor M71 steps whose union window takes at least
+  // this many 64-pixel slots (SMCDET_MH_BLOCK_SLOTS overrides, for A/Bs)
+  a.blk_slots = (flags & SMCDET_MH_NO_BLOCK) ? 0 : 5;
+  if (const char* e = getenv("SMCDET_MH_BLOCK_SLOTS")) a.blk_slots = atoi(e);
   if (a.m.model == SMCDET_MODEL_M71 && !full && !global_tile && !a.scalar_slots &&
       (flags & SMCDET_MH_PSF_TABLE)) {
     rc = psf_table_device(*model, a.m, st, &a.psf_tab, &a.tab_inv_h);

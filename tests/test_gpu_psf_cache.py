@@ -129,3 +129,62 @@ def test_psf_table_sweep_close_to_exp2_sweep():
     close = np.abs(res[0][2] - res[1][2])[same]
     assert close.max() < 2e-2, close.max()
     assert not all(np.array_equal(a, b) for a, b in zip(res[0], res[1]))
+
+
+NO_BLOCK = 16384  # include/smcdet_hip.h
+
+
+@pytest.mark.parametrize("H,W", [(32, 32), (24, 40), (40, 24)])
+def test_block_form_sweep_close_to_per_pixel_sweep(H, W):
+    """The block form of same-anchor M71 steps (the union window's first 16
+    rows / columns as a 16x16 block whose Gaussian PSF terms are one rank-4
+    MFMA) against the per-pixel form (SMCDET_MH_NO_BLOCK) on one sweep from
+    the same state with the same Philox draws: the profile is rounded
+    differently (a few ulp), so the decisions agree except at near ties, each
+    sweep's log-likelihood equals a fresh evaluation of its final state, each
+    persisted rate image equals a fresh render of it, and the two sweeps are
+    not bit-identical (the block path ran)."""
+    from smcdet_amd._rng import PhiloxStream
+    from smcdet_amd.images import M71ImageModel
+    from smcdet_amd.prior import M71Prior
+    N, K = 2048, 100
+    p = M71
+    model = M71ImageModel(image_height=H, image_width=W, background=p["background"],
+                          psf_radius=p["psf_radius"], adu_per_nmgy=p["adu_per_nmgy"],
+                          psf_params=p["psf_params"], noise_additive=p["noise_additive"],
+                          noise_multiplicative=p["noise_multiplicative"])
+
+    def prior(smin, smax, rate):
+        return M71Prior(min_objects=smin, max_objects=smax, counts_rate=rate, image_height=H,
+                        image_width=W, flux_alpha=p["flux_alpha"], flux_lower=p["flux_lower"],
+                        flux_upper=p["flux_upper"], pad=4)
+
+    torch.manual_seed(3)
+    _, l, f = prior(0, 40, 0.004).sample(num_catalogs=1, device=DEV)
+    img = model.sample(l, f)[0, 0, :, :, 0].contiguous()[None, None]
+    pr = prior(10, 10, 0.003125)
+    torch.manual_seed(8)
+    counts, locs, fluxes = pr.sample(num_tiles_per_side=1, stratify_by_count=True,
+                                     num_catalogs_per_count=N, device=DEV)
+    tau = torch.tensor([[0.05]], device=DEV)
+    res = []
+    for flags in (0, NO_BLOCK):
+        mh = p_m71_mh(K)
+        mh.debug_flags = flags
+        mh.rng = PhiloxStream(17)
+        rate = torch.empty(1, 1, N, H * W, device=DEV)
+        lo, fo, _ = mh.run(img, counts, locs, fluxes, tau, prior=pr, image_model=model,
+                           rate_out=rate)
+        ll = mh.last_loglik.cpu().numpy()
+        np.testing.assert_allclose(ll, model.loglikelihood(img, lo, fo).cpu().numpy(),
+                                   rtol=2e-6, atol=2e-3)
+        fresh = model.rate(lo, fo)[0, 0].permute(2, 0, 1).reshape(N, H * W)
+        np.testing.assert_allclose(rate[0, 0].cpu().numpy(), fresh.cpu().numpy(),
+                                   rtol=2e-5, atol=2e-3)
+        res.append((lo.cpu().numpy(), fo.cpu().numpy(), ll))
+    same = np.all(res[0][0] == res[1][0], axis=(-1, -2)) & np.all(res[0][1] == res[1][1], axis=-1)
+    assert same.mean() > 0.97, same.mean()
+    # the same final state: log-likelihoods (summed over each sweep's own
+    # rate image) as close as each is to a fresh evaluation
+    np.testing.assert_allclose(res[0][2][same], res[1][2][same], rtol=4e-6, atol=4e-3)
+    assert not all(np.array_equal(a, b) for a, b in zip(res[0], res[1]))
