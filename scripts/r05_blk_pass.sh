@@ -9,8 +9,8 @@ rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $D/pytest.log 
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 fi
 for tau in ${TAUS:-0.3}; do
-timeout -k 10 400 python scripts/mh_microbench.py --persist --variants ${VARIANTS:-blk0,blk5,blk4} \
-  --block-slots 0,4,5 --no-extra --rounds ${MB_ROUNDS:-9} --tau $tau > $D/mb_tau$tau.json 2>&1 || exit $?
+timeout -k 10 400 python scripts/mh_microbench.py --persist --variants ${VARIANTS:-blk0,blk5,blk-5} \
+  --block-slots 0,5,-5 --no-extra --rounds ${MB_ROUNDS:-9} --tau $tau > $D/mb_tau$tau.json 2>&1 || exit $?
 python3 -c "
 import json; s=open('$D/mb_tau$tau.json').read(); d=json.loads(s[s.index('{'):])['variants']
 for k,v in d.items(): print('tau $tau', k, 'median %.4f min %.4f ms' % (v['median_ms'], v['min_ms']))"
