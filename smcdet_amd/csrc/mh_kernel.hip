@@ -51,7 +51,14 @@ SMCDET_WAVE_TABLE
 constexpr int kMhWaves = 4;
 constexpr int kMhBlock = kMhWaves * kWave;
 constexpr int kSlots = 6;  // register-resident window passes (6*64 = 384 positions)
-constexpr int kBatch = 8;  // proposals computed together (3 lanes each)
+// proposals computed together (3 lanes each): 21 entries = 63 lanes.  A batch
+// is recomputed at its end and when an accepted move dirties a later entry's
+// source, so longer batches mean fewer recomputes (a simulation of the rule:
+// 0.145 -> 0.084 per iteration at acceptance 0.1, 0.183 -> 0.157 at 0.37) at
+// the same cost per recompute (SIMD lanes); results do not depend on it.
+// Same box (scripts/r05_batch_pass.sh): C4 MH launch 4.36 -> 4.26 ms, C2
+// microbench -1..-4% against 8 entries
+constexpr int kBatch = 21;
 
 struct MhArgs {
   DevModel m;
