@@ -964,7 +964,8 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
       constexpr bool kBlk = MODEL == SMCDET_MODEL_M71 && PPL > 1 && !GL && !TB && PAIRED;
       bool blk = false;
       if constexpr (kBlk)
-        blk = same && a.blk_slots > 0 && nslots >= a.blk_slots && r1 - r0 >= 15 && c1 - c0 >= 15;
+        blk = same && a.blk_slots > 0 && nslots >= a.blk_slots && r1 - r0 >= 15 && c1 - c0 >= 15 &&
+              r1 - r0 <= 16 && c1 - c0 <= 16;  // (the strip holds one row and one column: R <= 8)
       auto block = [&]() -> float {
         const int li = lane & 15, lk = lane >> 4;
         // MFMA operands: lane l is A[l & 15][l >> 4] and B[l >> 4][l & 15]

@@ -134,8 +134,8 @@ def test_psf_table_sweep_close_to_exp2_sweep():
 NO_BLOCK = 16384  # include/smcdet_hip.h
 
 
-@pytest.mark.parametrize("H,W", [(32, 32), (24, 40), (40, 24)])
-def test_block_form_sweep_close_to_per_pixel_sweep(H, W):
+@pytest.mark.parametrize("H,W,R", [(32, 32, 8), (24, 40, 8), (40, 24, 8), (32, 32, 9)])
+def test_block_form_sweep_close_to_per_pixel_sweep(H, W, R):
     """The block form of same-anchor M71 steps (the union window's first 16
     rows / columns as a 16x16 block whose Gaussian PSF terms are one rank-4
     MFMA) against the per-pixel form (SMCDET_MH_NO_BLOCK) on one sweep from
@@ -143,14 +143,16 @@ def test_block_form_sweep_close_to_per_pixel_sweep(H, W):
     differently (a few ulp), so the decisions agree except at near ties, each
     sweep's log-likelihood equals a fresh evaluation of its final state, each
     persisted rate image equals a fresh render of it, and the two sweeps are
-    not bit-identical (the block path ran)."""
+    not bit-identical (the block path ran).  R = 9 (19x19 windows, which the
+    block's one-row / one-column strip cannot hold) must take the per-pixel
+    form: identical results, rate images and log-likelihoods fresh."""
     from smcdet_amd._rng import PhiloxStream
     from smcdet_amd.images import M71ImageModel
     from smcdet_amd.prior import M71Prior
     N, K = 2048, 100
     p = M71
     model = M71ImageModel(image_height=H, image_width=W, background=p["background"],
-                          psf_radius=p["psf_radius"], adu_per_nmgy=p["adu_per_nmgy"],
+                          psf_radius=R, adu_per_nmgy=p["adu_per_nmgy"],
                           psf_params=p["psf_params"], noise_additive=p["noise_additive"],
                           noise_multiplicative=p["noise_multiplicative"])
 
@@ -187,4 +189,5 @@ def test_block_form_sweep_close_to_per_pixel_sweep(H, W):
     # the same final state: log-likelihoods (summed over each sweep's own
     # rate image) as close as each is to a fresh evaluation
     np.testing.assert_allclose(res[0][2][same], res[1][2][same], rtol=4e-6, atol=4e-3)
-    assert not all(np.array_equal(a, b) for a, b in zip(res[0], res[1]))
+    identical = all(np.array_equal(a, b) for a, b in zip(res[0], res[1]))
+    assert identical == (R != 8), identical
