@@ -124,6 +124,10 @@ __device__ __forceinline__ void tn_cache(float mu, float isig, float lb, float u
   lZ = nan_to_num(fast_log(normal_cdf(ub, mu, isig) - phl), 0.0f);
 }
 
+// the summed Hastings + prior term of an edge hit (-inf), tested on the
+// wave-uniform bits (a scalar compare, not a VALU float compare)
+__device__ __forceinline__ bool edge_hit(float hast) { return __float_as_uint(hast) == 0xff800000u; }
+
 // A proposal for one MH iteration: the chosen source j moves (h, w, f) ->
 // (hn, wn, fn).  Wave-uniform (SGPR) values.
 struct Proposal {
@@ -940,8 +944,8 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
         constexpr bool kFar = NSL > 1 && ns >= kSlots;
         if (kFar && npos > kSlots * kWave) dsum += far_positions(std::false_type{});
         dll = wave_sum(dsum);
-        accept = __builtin_amdgcn_readfirstlane((fmaf(tau, dll, P.hast) >= log_u) ? 1 : 0);
-        if (accept && P.hast != -INFINITY) {
+        accept = __builtin_amdgcn_ballot_w64(fmaf(tau, dll, P.hast) >= log_u) != 0;
+        if (accept && !edge_hit(P.hast)) {
 #pragma unroll
           for (int i = 0; i < ns; ++i)
             if (i < nslots) {
@@ -1029,7 +1033,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
         float dsum = 0.f;
         if (nslots == 1) dsum = same ? slots(I1{}, Same{}) : slots(I1{}, Win{});
         dll = wave_sum(dsum);
-        accept = __builtin_amdgcn_readfirstlane((fmaf(tau, dll, P.hast) >= log_u) ? 1 : 0);
+        accept = __builtin_amdgcn_ballot_w64(fmaf(tau, dll, P.hast) >= log_u) != 0;
       } else if (blk) {
         if constexpr (kBlk) {
           nslots = 5;  // (finish: the writes of s_*[0..5): 4 block pixels + the strip)
@@ -1090,7 +1094,7 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     // reproduced: U = 0 exactly with an edge hit (probability 2^-24 per hit),
     // where the reference accepts and its cached target becomes -inf, so it
     // accepts every later proposal of the sweep; here the sweep ends.
-    if (P.hast == -INFINITY) break;
+    if (edge_hit(P.hast)) break;
     if (accept) {
       if constexpr (FULL) {
         cur_ll = new_ll;
