@@ -33,6 +33,9 @@ VARIANTS = {
     "full": {"full_recompute": True},
     "unfused": {"fused": False, "stopping": "lockstep"},
     "refresh1": {"rate_refresh_every": 1},
+    # the MH sweep's per-pixel form everywhere (SMCDET_MH_NO_BLOCK): the
+    # block form's profile rounding vs the per-pixel one's
+    "no_block": {"debug_flags": 16384},
 }
 
 
@@ -53,6 +56,7 @@ def run(which, n_runs, variant, seed=777):
     v = dict(VARIANTS[variant])
     mh = SingleComponentMH(K, 0.1, 2.5, p["flux_lower"], p["flux_upper"],
                            full_recompute=v.pop("full_recompute", False))
+    mh.debug_flags = v.pop("debug_flags", 0)
     s = SMCsampler.from_tiles(tiles, prior, model, mh, N, cfg["rho"], cfg["method"],
                               p["flux_detection_threshold"], cfg.get("max_smc_iters", 1000),
                               print_every=10 ** 9, seed=seed, device=dev,
