@@ -960,11 +960,11 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
       // The 16x16 block form of a same-anchor step (M71; delta_from_dl2): the
       // block of the tile at (r0, c0) holds the union box's first 16 rows and
       // columns, the strip (one slot, s_*[4]) its 17th row and / or column.
-      // Taken where the box has at least 16 rows and columns and the
-      // per-pixel form would need a.blk_slots (default 5) slots: a same-box
-      // microbench at the C2 state measured the MH launch 4.7-5.2% faster
-      // with it there, and 1.2% faster where 4-slot boxes (16x16, or masked
-      // blocks of clipped boxes) took it too.
+      // Taken where the box has 16 or 17 rows and columns and the per-pixel
+      // form would need a.blk_slots (default 5) slots: a same-box microbench
+      // at the C2 state measured the MH launch 4.7-5.2% faster with it there;
+      // a first version that also took 4-slot boxes (16x16, and masked blocks
+      // of clipped boxes) gained only 1.2%.
       constexpr bool kBlk = MODEL == SMCDET_MODEL_M71 && PPL > 1 && !GL && !TB && PAIRED;
       bool blk = false;
       if constexpr (kBlk)
