@@ -1,0 +1,56 @@
+"""Count-posterior comparison of whole SMC runs at one configuration (test
+and bench helper; no oracle code, only recorded run summaries).
+
+Each run contributes its pruned-count histogram (the posterior over the number
+of detectable in-bounds stars after the final resample, sampler.py:198-219 and
+notebooks/smc.ipynb cell 9's summary) and its pruned posterior mean total flux
+(sampler.py:262-266 on the pruned fluxes).  Two samples of runs are compared
+by their per-bin means, the total variation between the mean histograms, and
+the mean pruned flux, each against the pooled standard error of the two means.
+
+Pre-registered gates (tests/test_gpu_statistical.py::test_c2_count_posterior,
+fixed in the commit that added them, before any GPU run of it):
+  * every bin: |mean_a - mean_b| <= 3 pooled SE;
+  * total variation <= 0.05 against the 648-run oracle target;
+  * pruned mean total flux within 3 pooled SE.
+`var_floor`: per-bin per-run variances that the target side's SE may not go
+below -- for the 20 reference runs, the 648-run oracle target's (20 runs of a
+law whose lower mode, ~13% of runs, carries most of bins 2-3 underestimate
+those bins' spread: the reference's own bin-2 mean sits 4.2 pooled SE from the
+oracle's, computed from the two fixtures alone).
+"""
+import numpy as np
+
+
+def hist_matrix(runs, nbins=11):
+    H = np.array([np.asarray(r["pruned_hist"], dtype=np.float64)[:nbins] for r in runs])
+    if H.shape[1] < nbins:
+        H = np.pad(H, ((0, 0), (0, nbins - H.shape[1])))
+    return H
+
+
+def count_posterior_compare(a_runs, b_runs, var_floor=None, nbins=11):
+    """a = the sampler under test, b = the target.  Returns a dict of the
+    statistics the gates read (plain floats / lists, JSON-serialisable)."""
+    Ha, Hb = hist_matrix(a_runs, nbins), hist_matrix(b_runs, nbins)
+    na, nb = len(Ha), len(Hb)
+    va, vb = Ha.var(0, ddof=1), Hb.var(0, ddof=1)
+    if var_floor is not None:
+        vb = np.maximum(vb, np.asarray(var_floor, dtype=np.float64)[:nbins])
+    se = np.sqrt(va / na + vb / nb)
+    d = Ha.mean(0) - Hb.mean(0)
+    z = np.where(se > 0, d / np.where(se > 0, se, 1.0), np.where(d == 0, 0.0, np.inf))
+    fa = np.array([r["mean_total_flux_pruned"] for r in a_runs], dtype=np.float64)
+    fb = np.array([r["mean_total_flux_pruned"] for r in b_runs], dtype=np.float64)
+    fse = float(np.sqrt(fa.var(ddof=1) / na + fb.var(ddof=1) / nb))
+    return {"n": [na, nb],
+            "hist_mean": Ha.mean(0).tolist(), "hist_mean_target": Hb.mean(0).tolist(),
+            "bin_z": z.tolist(), "max_abs_bin_z": float(np.max(np.abs(z))),
+            "total_variation": float(0.5 * np.abs(d).sum()),
+            "pruned_flux": float(fa.mean()), "pruned_flux_target": float(fb.mean()),
+            "pruned_flux_pooled_se": fse,
+            "pruned_flux_z": float((fa.mean() - fb.mean()) / fse) if fse > 0 else 0.0}
+
+
+def hist_var(runs, nbins=11):
+    return hist_matrix(runs, nbins).var(0, ddof=1)

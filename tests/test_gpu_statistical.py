@@ -77,6 +77,10 @@ def _run(which, cfg, image, seed, fused=True, persist=True):
                 ess_trace=esses, tau_trace=taus, final_ess=float(s.ess.flatten()[0]),
                 pruned_hist=hist / hist.sum(),
                 mean_total_flux=float(s.posterior_mean_total_flux(s.fluxes).flatten()[0]),
+                # sampler.py:198-219 then :262-266 (make_golden.py's statistic;
+                # the weights are uniform after the final resample)
+                mean_total_flux_pruned=float(
+                    s.posterior_mean_total_flux(s.pruned_fluxes).flatten()[0]),
                 # the oracle's statistic (make_oracle_stats.py): the plain mean
                 # over the final resampled population
                 mean_total_flux_unweighted=float(s.fluxes.sum(-1).mean()))
@@ -224,6 +228,44 @@ def test_statistical_parity_c2_geometry(which):
             lo, hi = np.quantile(boot, [0.0005, 0.9995])
             assert lo <= 0 <= hi, (np.median(a), np.median(b), lo, hi)
             assert mannwhitneyu(a, b).pvalue > 1e-3
+
+
+def test_c2_count_posterior():
+    """The headline configuration's scientific output (Missing #2):
+    the pruned-count posterior (number of detectable in-bounds stars,
+    sampler.py:198-219; notebooks/smc.ipynb cell 9 prints the reference's) and
+    the pruned posterior mean total flux (sampler.py:262-266), over 256 GPU
+    runs of SMCsampler at C2 (32x32 M71 tile, S = 10, N = 4096, K = 100,
+    systematic, rho = 0.5) against
+      * the 648 float64 oracle runs (stats_c2_moderate_4096_k100_oracle.json),
+      * the reference's own 20 runs (stats_c2_moderate_4096_k100.json).
+    Gates, pre-registered (tests/_stats.py; fixed before this test ran on a
+    GPU): every bin within 3 pooled SE of both targets (the reference side's
+    per-run variance floored at the oracle's, tests/_stats.py); total
+    variation <= 0.05 against the oracle target; pruned mean
+    total flux within 3 pooled SE of both."""
+    from tests._stats import count_posterior_compare, hist_var
+    orc = _load("c2_moderate_4096_k100_oracle")
+    ref = _load("c2_moderate_4096_k100")
+    cfg = ref["config"]
+    image = torch.tensor(ref["image"], dtype=torch.float32, device="cuda")
+    runs = [_run("c2_moderate_4096_k100", cfg, image, 5000 + i) for i in range(256)]
+    vs_orc = count_posterior_compare(runs, orc["runs"])
+    vs_ref = count_posterior_compare(runs, ref["runs"], var_floor=hist_var(orc["runs"]))
+    out = os.environ.get("SMCDET_STATS_OUT")
+    if out:
+        with open(out, "w") as f:
+            json.dump({"vs_oracle": vs_orc, "vs_reference": vs_ref}, f, indent=1)
+    for name, r in (("oracle", vs_orc), ("reference", vs_ref)):
+        print(name, "hist", np.round(r["hist_mean"], 4), "target",
+              np.round(r["hist_mean_target"], 4), "z", np.round(r["bin_z"], 2), "TV",
+              round(r["total_variation"], 4), "flux", r["pruned_flux"], r["pruned_flux_target"],
+              "z", round(r["pruned_flux_z"], 2))
+    for name, r in (("oracle", vs_orc), ("reference", vs_ref)):
+        assert r["max_abs_bin_z"] <= 3.0, (name, "bin", r["bin_z"])
+        assert abs(r["pruned_flux_z"]) <= 3.0, (name, "pruned flux", r["pruned_flux"],
+                                                r["pruned_flux_target"])
+    assert vs_orc["total_variation"] <= 0.05, ("TV vs oracle", vs_orc["total_variation"])
 
 
 def test_fused_run_equals_method_by_method_run():
