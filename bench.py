@@ -670,6 +670,27 @@ def vs_reference(dev, which="c2_moderate", n_runs=128):
         out[key] = {"ours": a, "reference": b,
                     "rel_diff": (a["mean"] - b["mean"]) / abs(b["mean"]),
                     "diff_in_pooled_se": (a["mean"] - b["mean"]) / pooled if pooled else None}
+    # the count posterior (sampler.py:198-219, 262-266): each run's pruned-count
+    # histogram and pruned mean total flux, compared as tests/_stats.py does
+    # (tests/test_gpu_statistical.py::test_c2_count_posterior's gates)
+    if all("pruned_hist" in r and "mean_total_flux_pruned" in r for r in rr):
+        from tests._stats import count_posterior_compare, hist_var
+        pc = s.pruned_counts.reshape(n_runs, -1)
+        hists = torch.stack([torch.bincount(pc[i], minlength=S + 1)[:S + 1] for i in range(n_runs)])
+        hists = (hists.double() / pc.shape[-1]).cpu().numpy()
+        pflux = s.posterior_mean_total_flux(s.pruned_fluxes).reshape(-1).double().cpu().numpy()
+        ours = [{"pruned_hist": h, "mean_total_flux_pruned": float(f)} for h, f in zip(hists, pflux)]
+        floor = None
+        if kind == "reference":
+            opath = os.path.join(ROOT, "tests", "golden", f"stats_{which}_oracle.json")
+            if os.path.exists(opath):
+                floor = hist_var(json.load(open(opath))["runs"], S + 1)
+        cp = count_posterior_compare(ours, rr, var_floor=floor, nbins=S + 1)
+        cp["gates"] = ("every bin within 3 pooled SE; TV <= 0.05 against the 648-run oracle "
+                       "target; pruned flux within 3 pooled SE" +
+                       ("; reference per-bin variance floored at the oracle's" if floor is not None
+                        else ""))
+        out["count_posterior"] = cp
     return out
 
 

@@ -20,26 +20,29 @@ by the oracle's float64 tile pass included.  From there on a twin is a new
 draw of the run's random outcome, so on "fragile" seeds (oracle log Z
 between the modes) the mode is not a function of the draws.
 
-The gates come from the round-5 evidence (profiles/r05/paired_c2_all.json:
-all 257 oracle runs replayed): the GPU and the oracle end in different modes
-in 14 of 257 pairs (5.4%; 8 GPU-lower-only, 6 oracle-lower-only, McNemar
-p = 0.79), the GPU and its own reference-arithmetic twin in 12 (4.7%), and
-the float32-class oracle and the float64 oracle in 15 of 191
-(scripts/mode_share.py) -- a discordance rate of ~5% is the chaos of
-near-tie decisions, whatever the two arithmetics.  The test checks:
+The null rate of mode discordance is ORACLE-ONLY evidence, frozen in round 6
+(pre-registered; never re-fitted to GPU replays): on the 276 seeds that both
+committed oracle targets hold, the float64 oracle and its float32-class build
+(same draws, stats_c2_moderate_4096_k100_oracle{,_f32}.json) end in different
+modes in 19 runs (10 : 9) -- the chaos of near-tie decisions between two
+arithmetics of the same algorithm, with no implementation under test in it
+(tests/test_oracle_paired.py::test_oracle_only_discordance_rate recomputes it
+from the fixtures).  The GPU-vs-oracle replays of rounds 4-5 (14 of 257, 30 of
+648) are supporting evidence only.  The test checks:
   * the pairing: ladders equal (|delta tau| <= 1e-5) for the first two
     iterations in >= 90% of runs;
   * agreement where runs are robust: the number of pairs in different modes
     (cut: median - 40 nats; the lower mode sits ~65-80 nats below) is
-    consistent with that 5.4% rate (one-sided binomial p > 0.001: at most 9
-    of the default 48), and median |delta log Z| <= 5 nats over the runs in
-    the same mode;
+    consistent with that oracle-only rate (one-sided binomial p > 0.001),
+    and median |delta log Z| <= 5 nats over the runs in the same mode;
   * no systematic excess: McNemar's exact test on the runs in different
     modes (GPU lower only vs oracle lower only), two-sided p > 0.01.
 The reference-arithmetic twin (SingleComponentMH(full_recompute=True)) is
 recorded next to it as a control (SMCDET_PAIRED_OUT summary).
 """
-DISCORDANCE = 14 / 257  # profiles/r05/paired_c2_all.json
+# FROZEN (round 6): the oracle-only discordance, float64 vs float32-class
+# oracle on their 276 common seeds.  Do not re-fit.
+DISCORDANCE = 19 / 276
 import json
 import os
 

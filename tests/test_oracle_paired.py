@@ -90,3 +90,28 @@ def paired_oracle_run(img, cfg, seed):
         tau, _ = O.temper(ll, tau, cfg["rho"] * N)
         W, ess, logZ = O.update_weights(ll, tau, tau_prev, logZ, N)
     return dict(logZ=float(logZ.flat[0]), iters=it)
+
+
+def test_oracle_only_discordance_rate():
+    """The paired C2 gate's frozen null rate (tests/test_gpu_paired.py
+    DISCORDANCE = 19/276): the float64 oracle and its float32-class build on
+    the seeds both committed targets hold end in different log Z modes (cut:
+    the common seeds' float64 median - 40 nats) in 19 of 276 runs, 10 : 9."""
+    import json
+    import os
+
+    from tests._params import GOLDEN
+    from tests.test_gpu_paired import DISCORDANCE
+
+    def logz(name):
+        with open(os.path.join(GOLDEN, name)) as f:
+            return {r["seed"]: r["logZ"] for r in json.load(f)["runs"]}
+    a = logz("stats_c2_moderate_4096_k100_oracle.json")
+    b = logz("stats_c2_moderate_4096_k100_oracle_f32.json")
+    common = sorted(set(a) & set(b))
+    la, lb = np.array([a[s] for s in common]), np.array([b[s] for s in common])
+    cut = np.median(la) - 40.0
+    x, y = la < cut, lb < cut
+    assert len(common) == 276
+    assert int((x & ~y).sum()) == 10 and int((~x & y).sum()) == 9
+    assert DISCORDANCE == int((x != y).sum()) / len(common)
