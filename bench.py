@@ -778,19 +778,36 @@ def workload_leg(args, dev, rank, world, dist, backend, name):
         a2.workload, a2.total_tiles, a2.tiles_per_gpu = "c2", 8, 1
     else:
         a2.workload, a2.total_tiles, a2.tiles_per_gpu = name, 0, 42
-    s, _, steps_per_step, _, cfg = build_sampler(a2, dev, rank)
-    s.fused_step = False
-    s.initialize()
-    s._temper_reweight(with_resample=True)
-
-    def step():
-        idx, s._pending_idx = s._pending_idx, None
-        s._step(idx)
-
     steps = max(3, min(args.steps, 10))
-    for _ in range(2):
-        step()
-    _sync()
+    # everything that can fail on one rank alone (the sampler's build, its
+    # allocations, the warm-up steps) happens before the leg's first
+    # collective, and the ranks agree on the outcome first: a failed rank
+    # makes every rank skip the leg instead of leaving the others blocked in
+    # its barrier
+    err = None
+    try:
+        s, _, steps_per_step, _, cfg = build_sampler(a2, dev, rank)
+        s.fused_step = False
+        s.initialize()
+        s._temper_reweight(with_resample=True)
+
+        def step():
+            idx, s._pending_idx = s._pending_idx, None
+            s._step(idx)
+
+        for _ in range(2):
+            step()
+        _sync()
+    except Exception as e:  # reported, after the ranks agree
+        err = repr(e)
+    if dist:
+        ok = torch.tensor([0 if err else 1], dtype=torch.int32,
+                          device=dev if backend == "nccl" else "cpu")
+        tdist.all_reduce(ok, op=tdist.ReduceOp.MIN)
+        if int(ok) == 0 and err is None:
+            err = "skipped: the leg failed on another rank"
+    if err is not None:
+        return {"error": err}
     if dist:
         tdist.barrier()
     _sync()
@@ -878,6 +895,20 @@ def _hip_fused(s):
         _hip.ref(s.ImageModel._cmodel()), int(s.counts.shape[-1]), int(s.locs.shape[-2]), flags))
 
 
+def launch_ranks(n):
+    """The driver's multi-GPU command (torch.distributed.run, one rank per GPU,
+    rendezvous on 127.0.0.1) with this process's arguments, as a child."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     global REHEARSAL
     args = parse()
@@ -885,6 +916,15 @@ def main():
         REHEARSAL = True
         os.environ["SMCDET_DIST_BACKEND"] = "gloo"
         args.no_kernel_timing = args.no_full_run = args.no_cpu_baseline = True
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start the driver's
+        # torchrun command as a CHILD process (nothing has touched the GPU in
+        # this process: no exec from a GPU-initialised process) and exit with
+        # its status
+        sys.exit(launch_ranks(args.gpus))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started "
+                         f"WORLD_SIZE={os.environ['WORLD_SIZE']} ranks; they must agree")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -247,6 +247,14 @@ class _Checked:
     def __getattr__(self, k):
         return getattr(self._fn, k)
 
+    def __setattr__(self, k, v):
+        # argtypes / restype (e.g. scripts/trace_phases.py) belong to the
+        # ctypes function itself, not to this wrapper
+        if k in ("_fn", "_name"):
+            object.__setattr__(self, k, v)
+        else:
+            setattr(self._fn, k, v)
+
 
 class _Lib:
     """libsmcdet_hip.so with alias-checked entry points (check_aliases);

@@ -968,8 +968,9 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
       constexpr bool kBlk = MODEL == SMCDET_MODEL_M71 && PPL > 1 && !GL && !TB && PAIRED;
       bool blk = false;
       if constexpr (kBlk)
-        blk = same && a.blk_slots > 0 && nslots >= a.blk_slots && r1 - r0 >= 15 && c1 - c0 >= 15 &&
-              r1 - r0 <= 16 && c1 - c0 <= 16;  // (the strip holds one row and one column: R <= 8)
+        blk = same && a.blk_slots > 0 && m.R <= 8 && nslots >= a.blk_slots && r1 - r0 >= 15 &&
+              c1 - c0 >= 15 && r1 - r0 <= 16 && c1 - c0 <= 16;  // (the strip holds one row and one
+                                                                 // column: R <= 8, clipped or not)
       auto block = [&]() -> float {
         const int li = lane & 15, lk = lane >> 4;
         // MFMA operands: lane l is A[l & 15][l >> 4] and B[l >> 4][l & 15]
@@ -1649,7 +1650,11 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
   // the block form for same-anchor M71 steps whose union window takes at least
   // this many 64-pixel slots (SMCDET_MH_BLOCK_SLOTS overrides, for A/Bs)
   a.blk_slots = (flags & SMCDET_MH_NO_BLOCK) ? 0 : 5;
+#ifdef SMCDET_DIAG
+  // (diagnostic build only: A/B thresholds of scripts/mh_microbench.py; the
+  // product never reads the environment on the launch path)
   if (const char* e = getenv("SMCDET_MH_BLOCK_SLOTS")) a.blk_slots = atoi(e);
+#endif
   if (a.m.model == SMCDET_MODEL_M71 && !full && !global_tile && !a.scalar_slots &&
       (flags & SMCDET_MH_PSF_TABLE)) {
     rc = psf_table_device(*model, a.m, st, &a.psf_tab, &a.tab_inv_h);

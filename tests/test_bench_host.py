@@ -96,3 +96,65 @@ def test_torchrun_two_ranks_default_line_with_c3_leg_and_gather():
     assert g["backend"] == "gloo"
     assert g["gathered_shape_locs"] == [8, 8, d["config"]["particles"], 10, 2]
     assert g["bytes_per_rank"] > 0
+
+
+def test_torchrun_eight_ranks_default_line():
+    """The driver's N = 8 command, rehearsed on the CPU: one tile per rank
+    (weak scaling), MAX over ranks (rank 7 sleeps 8 ms per step), the C3 leg at
+    8 tiles per rank with its catalog gather to [8, 8, ...] on rank 0, and the
+    rank-0-only fields."""
+    d = _torchrun_rehearsal(["--steps", "3"], world=8)
+    assert d["n_gpus"] == 8 and d["scaling"] == "weak"
+    assert d["ms_per_step"] >= 8.0 * 0.95, d["ms_per_step"]
+    np_ = d["config"]["particles"] * d["config"]["mh_iters"]
+    assert abs(d["value"] - 8 * np_ / (d["ms_per_step"] * 1e-3)) <= 1e-6 * d["value"]
+    c3 = d["c3_strong"]
+    assert c3["n_gpus"] == 8 and c3["config"]["tiles_per_gpu_rank0"] == 8
+    # rank 7: 8 tiles x 8 ms per step
+    assert c3["ms_per_step"] >= 64.0 * 0.95, c3["ms_per_step"]
+    assert c3["catalog_gather"]["gathered_shape_locs"] == [8, 8, d["config"]["particles"], 10, 2]
+    assert "cpu_baseline" not in d
+    assert d["smc"]["vs_reference"]["rehearsal"].endswith("on rank 0")
+
+
+def test_torchrun_seven_ranks_uneven_c3_shares():
+    """64 tiles over 7 ranks: rank 0 owns 10 tiles, ranks 1..6 own 9
+    (bench.shard = distributed.shard_tiles); the MAX over ranks is rank 6's
+    9 tiles x 7 ms per step, and value counts all 64 tiles."""
+    d = _torchrun_rehearsal(["--total-tiles", "64", "--no-c3", "--steps", "3"], world=7)
+    assert d["n_gpus"] == 7 and d["scaling"] == "strong"
+    assert d["config"]["tiles_per_gpu"] == 10
+    assert [len(bench.shard(64, 7, r)) for r in range(7)] == [10] + [9] * 6
+    assert d["ms_per_step"] >= 63.0 * 0.95, d["ms_per_step"]
+    np_ = d["config"]["particles"] * d["config"]["mh_iters"]
+    assert abs(d["value"] - 64 * np_ / (d["ms_per_step"] * 1e-3)) <= 1e-6 * d["value"]
+
+
+def test_gpus_flag_launches_ranks_as_a_child():
+    """`python bench.py --gpus 2` without torchrun starts the driver's torchrun
+    command as a child process (bench.launch_ranks) and prints its one line."""
+    import json
+    import subprocess
+    env = dict(os.environ, SMCDET_DIST_BACKEND="gloo", OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--host-rehearsal", "--particles", "64", "--steps", "3", "--warmup", "1",
+                        "--no-c3"], env=env, cwd=ROOT, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    assert json.loads(lines[0])["n_gpus"] == 2
+
+
+def test_gpus_flag_mismatch_fails_loudly():
+    """A launcher's WORLD_SIZE that disagrees with --gpus is an error (exit
+    status != 0, message on stderr), never a silent one-rank line."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--host-rehearsal"], env=env, cwd=ROOT, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode != 0
+    assert "--gpus 2" in r.stderr and "WORLD_SIZE=3" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

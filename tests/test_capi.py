@@ -184,3 +184,18 @@ def test_ptr_temporaries_released_after_the_call():
     assert len(_hip._kept()) <= _hip._KEEP_MAX
     L.smcdet_launch_timing(0)
     assert len(_hip._kept()) == 0
+
+
+def test_checked_wrapper_forwards_argtypes():
+    """Attribute writes on an entry point reach the ctypes function (ADVICE r5:
+    scripts/trace_phases.py sets argtypes through _hip.lib()); checked on a
+    libc function so the library's own signatures stay untouched."""
+    import ctypes
+
+    from smcdet_amd import _hip
+    raw = ctypes.CDLL(None).strlen
+    w = _hip._Checked(raw, "smcdet_test_strlen")
+    w.argtypes = [ctypes.c_char_p]
+    w.restype = ctypes.c_size_t
+    assert raw.argtypes == [ctypes.c_char_p] and raw.restype is ctypes.c_size_t
+    assert w(b"graft") == 5
