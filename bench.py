@@ -57,6 +57,13 @@ PMC_FILE = "pmc_mh_r05.json"
 # the same for the C4 / C5 MH launches (the default run's `c4` / `c5` legs)
 PMC_FILES = {"c2": PMC_FILE, "c4": "pmc_mh_c4_r05.json", "c5": "pmc_mh_c5_r05.json"}
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions/s: 1 per SIMD per 4 cycles (measured 4.2)
+# The issue floor of the VALU stream, calibrated at the MH sweeps' occupancies
+# (scripts/probe/issue_probe.hip: s_memtime cycles of 1..8 waves per SIMD,
+# profiles/r06/issue_probe.txt): SIMD cycles per non-transcendental VALU
+# wave-instruction; transcendentals are counted as co-issued (free), so the
+# floor is a lower bound on the cycles any instruction mix with those counts
+# needs
+ISSUE_MODEL = {"plain": 4.0, "trans": 0.0, "probe": "profiles/r06/issue_probe.txt"}
 # measured SIMD issue cycles per wave-instruction (scripts/probe/isa_probe.hip, 4 waves/SIMD,
 # profiles/r01_s2_isa_probe.txt): plain VALU 4.2, transcendental 8.6, packed f32 6.0
 ISSUE_CYC_VALU, ISSUE_CYC_TRANS = 4.2, 8.6
@@ -542,6 +549,43 @@ def pmc_summary(args):
     return d, f"profiles/{fname}"
 
 
+def roofline_valu(args, mh_rate, f_alg, launch_steps, mh_ms):
+    """The binding resource's roofline (FP32 VALU, the MH sweep
+    is not HBM-bound): achieved = §8d's 68.04 kFLOP per particle-step of the
+    reference's full re-render x the sweep's particle-steps/s over the timed
+    steps' own launches, against the FP32 vector peak.  `issue`: the executed
+    instruction stream against the calibrated issue floor (ISSUE_MODEL,
+    scripts/probe/issue_probe.hip at 4 and 7 waves per SIMD): the PMC pass's
+    VALU wave-instructions per particle-step, non-transcendental ones at
+    ISSUE_MODEL["plain"] cycles each, transcendentals co-issued (free), over
+    the SIMD cycles the launch had per particle-step at its measured clock."""
+    tf = mh_rate * f_alg / 1e12
+    out = {"bound": "valu", "achieved": tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+           "frac": tf / FP32_PEAK_TFLOPS, "alg_flop_per_particle_step": f_alg,
+           "kernel_ms": mh_ms,
+           "note": "reference-equivalent FLOPs (SURVEY §8d: the full re-render the reference "
+                   "executes per particle-step); the incremental sweep executes fewer"}
+    d, src = pmc_summary(args)
+    if d is None:
+        out["issue"] = {"omitted": src}
+        return out
+    try:
+        ps = d["per_particle_step"]
+        valu, trans = ps["SQ_INSTS_VALU"], ps.get("SQ_INSTS_VALU_TRANS_F32") or 0.0
+        clk = (d.get("effective_clock") or {}).get("ghz") or 2.4
+        avail = 256 * 4 * clk * 1e9 * mh_ms * 1e-3 / launch_steps
+        floor = ISSUE_MODEL["plain"] * (valu - trans)
+        out["issue"] = {"valu_wave_insts_per_particle_step": valu,
+                        "trans_wave_insts_per_particle_step": trans,
+                        "floor_cycles_per_particle_step": floor,
+                        "available_cycles_per_particle_step": avail, "clock_ghz": clk,
+                        "issue_frac": floor / avail, "cycles_per_valu_inst": avail / valu,
+                        "model": ISSUE_MODEL, "source": src}
+    except Exception as e:  # never fail the bench line on it
+        out["issue"] = {"error": repr(e)}
+    return out
+
+
 def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
     """The binding resource (FP32 VALU issue).  reference_equivalent: SURVEY
     §8d's FLOPs of the reference's full re-render per particle-step, which the
@@ -964,6 +1008,16 @@ def main():
     s, mh, steps_per_step, cpu_tile, cfg = build_sampler(args, dev, rank)
     s.fused_step = args.fused_step
     s.ancestor_bins = not args.ancestor_indices
+    # the random streams' state before the run: restart() reruns the identical
+    # workload (Philox-keyed draws: same proposals, decisions, ladder)
+    rng0 = dict(s.rng.state()) if hasattr(s, "rng") else None
+
+    def restart():
+        if rng0 is not None:
+            s.rng.load_state(rng0)
+        s.initialize()
+        s._temper_reweight(with_resample=True)
+
     s.initialize()
     cfg = dict(cfg, ancestors="indices" if args.ancestor_indices else "bins")
     cfg = dict(cfg, step="two launches" if not args.fused_step else (
@@ -1004,8 +1058,7 @@ def main():
                 step()
             n_pw += 10
             _sync()
-        s.initialize()
-        s._temper_reweight(with_resample=True)
+        restart()
         prewarm = {"seconds": round(time.perf_counter() - t_pw, 3), "steps": n_pw,
                    "note": "untimed back-to-back steps before the warmup steps (the chip's "
                            "clock ramps up over its first ~60 busy steps after idle: C2 sweep "
@@ -1025,28 +1078,51 @@ def main():
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
-    # The roofline's kernel duration: the next `steps` SMC steps again, each
-    # sweep launch timed by HIP events stamped on its own dispatch packet
-    # (hipExtLaunchKernel, smcdet_launch_timing).  Not inside the timed
-    # region: any per-launch timing (these events or hipEventRecord markers)
-    # leaves a 7-10 us bubble before the next launch (rocprofv3 kernel traces,
-    # profiles/r02_s3_gap_bench.txt), while untimed back-to-back launches run
-    # gap-free.
-    starts = []
+    end_state = [x.detach().clone() for x in (s.log_normalizing_constant, s.temperature,
+                                              s.locs)] if not REHEARSAL else None
+    # The roofline's kernel durations describe the TIMED steps themselves: the
+    # sampler restarts from the same random-stream state and replays the
+    # identical W warmup + K timed SMC iterations (same draws, decisions and
+    # temperature ladder; replay_identical checks the end state bit for bit),
+    # this time with every launch of the K steps timed by HIP events stamped
+    # on its own dispatch packet (hipExtLaunchKernel, smcdet_launch_timing):
+    # the MH sweep and the per-tile temper / reweight / resampling pass.  Not
+    # inside the timed region: per-launch timing leaves a 7-10 us bubble
+    # before the next launch (profiles/r02_s3_gap_bench.txt), while untimed
+    # back-to-back launches run gap-free.
+    starts, tile_ev, replay = [], [], None
     if args.no_kernel_timing:
         ev = [elapsed * 1e3 / args.steps]
     else:
-        _hip.launch_timing(args.steps)
+        restart()
+        for _ in range(args.warmup):
+            step()
+        _sync()
+        _hip.launch_timing(2 * args.steps)
+        _hip.launch_timing_tiles(True)
+        t1 = time.perf_counter()
         for _ in range(args.steps):
             step()
         _sync()
-        ev = _hip.launch_timing_read(args.steps)
-        starts = _hip.launch_timing_starts(args.steps)
+        replay_s = time.perf_counter() - t1
+        ev_all = _hip.launch_timing_read(2 * args.steps)
+        st_all = _hip.launch_timing_starts(2 * args.steps)
         _hip.launch_timing(0)
-    # step-time spread (untimed): the same steps in 3 more bracketed passes,
-    # and the launch-to-launch intervals of the timing pass above
+        if len(ev_all) == 2 * args.steps:  # two launches per step: sweep, tile pass
+            ev, tile_ev, starts = ev_all[0::2], ev_all[1::2], st_all[0::2]
+        else:                              # fused step: one launch per step
+            ev, starts = ev_all, st_all
+        same = all(torch.equal(a_, b_) for a_, b_ in zip(
+            end_state, (s.log_normalizing_constant, s.temperature, s.locs)))
+        replay = {"ms_per_step": replay_s / args.steps * 1e3, "replay_identical": bool(same),
+                  "launches_timed": len(ev_all)}
+    # step-time spread (untimed): the same W + K steps replayed 3 more times,
+    # each bracketed like the timed region
     passes = []
     for _ in range(0 if args.no_spread else 3):
+        restart()
+        for _ in range(args.warmup):
+            step()
         _sync()
         t1 = time.perf_counter()
         for _ in range(args.steps):
@@ -1113,9 +1189,11 @@ def main():
                      "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": f"smcdet {args.kernel}_sweep_kernel", "kernel_ms": mh_ms,
                      "kernel_timing": ("step time (no timing pass)" if args.no_kernel_timing
-                                       else f"HIP dispatch events, {len(ev)} launches right "
-                                            "after the timed region"),
+                                       else f"HIP dispatch events on the {len(ev)} sweep "
+                                            "launches of the timed steps, replayed identically "
+                                            "(step_attribution)"),
                      "alg_bytes_per_particle_step": b_alg},
+        "roofline_valu": roofline_valu(args, mh_rate, f_alg, launch_steps, mh_ms),
         "compute": compute_block(args, mh_rate, f_alg, launch_steps, mh_ms),
         "smc": {"temperature_min": float(s.temperature.min()),
                 "acc_rate": float(s.mutation_acc_rates.mean()),
@@ -1135,8 +1213,21 @@ def main():
         "repeat_passes_ms_per_step": passes,
         "launch_interval_ms": pct(_np.diff(starts)) if len(starts) > 1 else None,
         "kernel_ms": pct(ev),
-        "note": "untimed: 3 more bracketed passes of the same steps; sweep-launch start-to-start "
-                "intervals and durations from the dispatch-stamped timing pass"}
+        "note": "untimed: the timed steps replayed 3 more times, each bracketed like the timed "
+                "region; sweep-launch start-to-start intervals and durations from the "
+                "dispatch-stamped replay"}
+    if replay is not None:
+        # ms_per_step = sweep + tile pass + the rest (launch gaps, host enqueue
+        # stalls), all over the timed steps' own workload
+        sw_ms = mh_ms
+        tl_ms = sum(tile_ev) / len(tile_ev) if tile_ev else 0.0
+        step_ms = elapsed / args.steps * 1e3
+        out["step_attribution"] = dict(
+            replay, timed_ms_per_step=step_ms, sweep_ms=sw_ms, tile_pass_ms=tl_ms,
+            gap_ms=step_ms - sw_ms - tl_ms, tile_pass_kernel_ms=pct(tile_ev),
+            note="the timed region's W warmup + K SMC iterations replayed from the same "
+                 "random-stream state with every sweep and tile-pass launch of the K steps "
+                 "timed on its dispatch packet; gap = timed ms/step - sweep - tile pass")
     if c3 is not None:
         out["c3_strong"] = c3
     out.update(legs)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SMCDET_ABI_VERSION 17
+#define SMCDET_ABI_VERSION 18
 
 /* status codes */
 #define SMCDET_OK 0
@@ -185,6 +185,13 @@ int smcdet_launch_timing_read(float* ms, int32_t max, int32_t* n_out);
 /* The same launches' start times in ms after the first timed launch's start
  * (launch-to-launch intervals: the step-time spread bench.py reports). */
 int smcdet_launch_timing_starts(float* ms, int32_t max, int32_t* n_out);
+/* on != 0: while timing is enabled, the per-tile temper / reweight /
+ * resampling launches (smcdet_temper, smcdet_update_weights,
+ * smcdet_temper_reweight and the tile pass of a two-launch
+ * smcdet_mh_sweep_step) also take event pairs from the pool, in launch order
+ * with the sweeps (a two-launch SMC step: sweep, then tile pass).  Off by
+ * default; smcdet_launch_timing(0) turns it off. */
+int smcdet_launch_timing_tiles(int32_t on);
 
 /* ImageModel.loglikelihood / M71ImageModel.loglikelihood
  * (smcdet/images.py:85-102, :159-175): out[T,N].  Tiles up to 4096 pixels

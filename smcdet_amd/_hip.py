@@ -25,7 +25,7 @@ SMCDET_RESAMPLE_SYSTEMATIC = 1
 SMCDET_MH_FULL_RECOMPUTE = 1
 SMCDET_MH_COMPONENT_BY_COUNT = 2
 SMCDET_MH_SKIP_DONE = 4
-ABI_VERSION = 17
+ABI_VERSION = 18
 SMCDET_SMC_FREEZE_DONE = 1
 SMCDET_SMC_TWO_LAUNCH = 2
 
@@ -120,6 +120,7 @@ _SIGS = {
     "smcdet_launch_timing": ([c_i], c_i),
     "smcdet_launch_timing_read": ([c_p, c_i, c_p], c_i),
     "smcdet_launch_timing_starts": ([c_p, c_i, c_p], c_i),
+    "smcdet_launch_timing_tiles": ([c_i], c_i),
     "smcdet_last_error": ([], ctypes.c_char_p),
     "smcdet_loglik": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
     "smcdet_render": ([c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_p], c_i),
@@ -394,6 +395,12 @@ def launch_timing_starts(max_launches: int):
     check(lib().smcdet_launch_timing_starts(ctypes.addressof(buf), int(max_launches),
                                             ctypes.byref(n)), "smcdet_launch_timing_starts")
     return [float(buf[i]) for i in range(min(n.value, int(max_launches)))]
+
+
+def launch_timing_tiles(on: bool):
+    """Also time the per-tile temper / reweight / resampling launches, in launch
+    order with the sweeps (smcdet_launch_timing_tiles)."""
+    check(lib().smcdet_launch_timing_tiles(1 if on else 0), "smcdet_launch_timing_tiles")
 
 
 # ptr() keeps the tensors it converts alive until the next library call made

@@ -38,6 +38,9 @@ int ensure_lds(const void* kernel, size_t bytes) {
 // ---- launch timing pool (smcdet_launch_timing / _read) ----------------------
 static hipEvent_t* g_tev = nullptr;  // 2 * g_tcap events: (start, stop) per launch
 static int g_tcap = 0, g_tused = 0;
+static bool g_ttiles = false;  // smcdet_launch_timing_tiles
+
+bool timing_tiles() { return g_ttiles && g_tused < g_tcap; }
 
 bool timing_next(hipEvent_t* start, hipEvent_t* stop) {
   if (g_tused >= g_tcap) return false;
@@ -52,6 +55,7 @@ static void timing_free() {
   delete[] g_tev;
   g_tev = nullptr;
   g_tcap = g_tused = 0;
+  g_ttiles = false;
 }
 
 int validate_model(const smcdet_image_model_t* m, int max_pixels) {
@@ -182,6 +186,11 @@ int smcdet_launch_timing_starts(float* ms, int32_t max, int32_t* n_out) {
       return smcdet::set_error(SMCDET_EHIP, "launch %d: event timing failed", i);
   }
   if (n_out) *n_out = smcdet::g_tused;
+  return SMCDET_OK;
+}
+
+int smcdet_launch_timing_tiles(int32_t on) {
+  smcdet::g_ttiles = on != 0;
   return SMCDET_OK;
 }
 

@@ -90,6 +90,9 @@ int ensure_lds(const void* kernel, size_t bytes);
 // launch timing (smcdet_launch_timing): the next start / stop event pair of
 // the pool, or false (nulls) when timing is off or the pool is used up
 bool timing_next(hipEvent_t* start, hipEvent_t* stop);
+// the per-tile passes are timed too (smcdet_launch_timing_tiles) and the pool
+// has room
+bool timing_tiles();
 // A sweep launch whose timing events (if any) ride on its own dispatch packet
 // (hipExtLaunchKernel): no marker packet between kernels, so timing does not
 // open a launch bubble in the step it measures.

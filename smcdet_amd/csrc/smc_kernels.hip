@@ -352,7 +352,12 @@ int launch_tile(const TileArgs& a, hipStream_t st) {
   int rc = ensure_lds(fn, lds + sizeof(TileRed));
   if (rc) return rc;
   void* args[] = {const_cast<TileArgs*>(&a)};
-  hipError_t e = hipLaunchKernel(fn, dim3(a.T), dim3(nt), args, lds, st);
+  hipError_t e;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (timing_tiles() && timing_next(&e0, &e1))  // events on the dispatch packet (launch_sweep)
+    e = hipExtLaunchKernel(fn, dim3(a.T), dim3(nt), args, lds, st, e0, e1, 0);
+  else
+    e = hipLaunchKernel(fn, dim3(a.T), dim3(nt), args, lds, st);
   if (e != hipSuccess) return set_error(SMCDET_EHIP, "tile kernel launch: %s", hipGetErrorString(e));
   return check_launch("smcdet tile kernel");
 }
