@@ -73,6 +73,11 @@ SIMD_CYCLES_PER_S = 256 * 4 * 2.4e9
 REFERENCE_CPU = {"value": 8466.0, "unit": "particle-steps/sec", "cores": 8, "kind": "reference",
                  "sample": "reference SingleComponentMH, 32x32, N=4096, S=10, 10 iterations at "
                            "tau=0.3, torch 2.10 CPU float32 (SURVEY.md §6)"}
+# Cross-calibration of the port against the reference on the same 8 cores, the
+# same state and configuration (scripts/cpu_crosscal.py in the build container,
+# profiles/r06/cpu_crosscal.json): the port's particle-steps/s over the
+# reference's.  Converts the box's port figure to a reference-equivalent one.
+CROSSCAL_FILE = "profiles/r06/cpu_crosscal.json"
 
 
 # --host-rehearsal: the multi-rank bookkeeping on the CPU (gloo, stub sampler)
@@ -1268,6 +1273,17 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args, cpu_tile.cpu().numpy(),
                                                args.cpu_baseline_seconds)
             out["cpu_baseline"]["reference_measured"] = REFERENCE_CPU
+            cc = json.load(open(os.path.join(ROOT, CROSSCAL_FILE)))
+            r = cc["port_over_reference"]
+            out["cpu_baseline"]["calibration"] = {
+                "port_over_reference": r,
+                "reference_equivalent_value": out["cpu_baseline"]["value"] / r,
+                "reference_8_threads_same_container": cc["reference"]["particle_steps_per_s"],
+                "port_8_threads_same_container": cc["port"]["particle_steps_per_s"],
+                "source": CROSSCAL_FILE,
+                "note": "the reference's SingleComponentMH and this port on the same 8 cores "
+                        "(build container; the reference does not travel to the GPU box); "
+                        "reference_equivalent_value = this box's port rate / port_over_reference"}
         except Exception as e:  # report, never fail the bench line on it
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:
