@@ -56,18 +56,44 @@ F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
 PMC_FILE = "pmc_mh_r05.json"
 # the same for the C4 / C5 MH launches (the default run's `c4` / `c5` legs)
 PMC_FILES = {"c2": PMC_FILE, "c4": "pmc_mh_c4_r05.json", "c5": "pmc_mh_c5_r05.json"}
-VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions/s: 1 per SIMD per 4 cycles (measured 4.2)
-# The issue floor of the VALU stream, calibrated at the MH sweeps' occupancies
-# (scripts/probe/issue_probe.hip: s_memtime cycles of 1..8 waves per SIMD,
-# profiles/r06/issue_probe.txt): SIMD cycles per non-transcendental VALU
-# wave-instruction; transcendentals are counted as co-issued (free), so the
-# floor is a lower bound on the cycles any instruction mix with those counts
-# needs
-ISSUE_MODEL = {"plain": 4.0, "trans": 0.0, "probe": "profiles/r06/issue_probe.txt"}
-# measured SIMD issue cycles per wave-instruction (scripts/probe/isa_probe.hip, 4 waves/SIMD,
-# profiles/r01_s2_isa_probe.txt): plain VALU 4.2, transcendental 8.6, packed f32 6.0
-ISSUE_CYC_VALU, ISSUE_CYC_TRANS = 4.2, 8.6
-SIMD_CYCLES_PER_S = 256 * 4 * 2.4e9
+# The VALU issue costs on gfx950, measured at the MH sweeps' occupancies
+# (scripts/probe/issue_probe.hip: per-SIMD s_memtime spans of 16 independent
+# chains per wave, profiles/r06/issue_probe.txt): SIMD cycles per
+# wave-instruction at 4 waves per SIMD (the 32x32 sweep) and 7 (the 8x8
+# sweep).  Transcendentals are NOT co-issued (a 6 fma : 1 exp mix costs more
+# than the sum of its parts), and v_pk_* f32 ops cost ~1.85 plain ones.
+ISSUE_MODEL = {
+    "cycles": {"4": {"plain": 2.68, "packed": 4.94, "trans": 8.58},
+               "7": {"plain": 2.40, "packed": 4.45, "trans": 8.33}},
+    "floor": "plain x (VALU - TRANS) + trans x TRANS: packed ops counted as plain, so a lower "
+             "bound on the SIMD cycles the counted stream needs",
+    "probe": "profiles/r06/issue_probe.txt"}
+SIMDS = 256 * 4
+
+
+def waves_per_simd(tile):
+    """The MH sweep's occupancy: 7 waves per SIMD for tiles of <= 64 pixels
+    (mh_waves_per_eu<1>), 4 otherwise."""
+    return 7 if tile * tile <= 64 else 4
+
+
+def issue_floor(per_step, tile, clk_ghz, mh_ms, launch_steps):
+    """The calibrated issue floor of the PMC-counted VALU stream against the
+    SIMD cycles the launch had (at its measured clock), per particle-step."""
+    w = str(waves_per_simd(tile))
+    c = ISSUE_MODEL["cycles"][w]
+    valu = per_step["SQ_INSTS_VALU"]
+    trans = per_step.get("SQ_INSTS_VALU_TRANS_F32") or 0.0
+    floor = c["plain"] * (valu - trans) + c["trans"] * trans
+    avail = SIMDS * clk_ghz * 1e9 * mh_ms * 1e-3 / launch_steps
+    return {"waves_per_simd": int(w), "valu_wave_insts_per_particle_step": valu,
+            "trans_wave_insts_per_particle_step": trans,
+            "floor_cycles_per_particle_step": floor,
+            "available_cycles_per_particle_step": avail, "clock_ghz": clk_ghz,
+            "issue_frac": floor / avail, "cycles_per_valu_inst": avail / valu,
+            "costs": c}
+
+
 # the reference itself (torch CPU, smcdet/kernel.py) on the same workload, SURVEY §6 (build
 # container, 8 cores; the reference does not travel to the GPU box)
 REFERENCE_CPU = {"value": 8466.0, "unit": "particle-steps/sec", "cores": 8, "kind": "reference",
@@ -554,16 +580,15 @@ def pmc_summary(args):
     return d, f"profiles/{fname}"
 
 
-def roofline_valu(args, mh_rate, f_alg, launch_steps, mh_ms):
+def roofline_valu(args, mh_rate, f_alg, launch_steps, mh_ms, tile):
     """The binding resource's roofline (FP32 VALU, the MH sweep
     is not HBM-bound): achieved = §8d's 68.04 kFLOP per particle-step of the
     reference's full re-render x the sweep's particle-steps/s over the timed
     steps' own launches, against the FP32 vector peak.  `issue`: the executed
-    instruction stream against the calibrated issue floor (ISSUE_MODEL,
-    scripts/probe/issue_probe.hip at 4 and 7 waves per SIMD): the PMC pass's
-    VALU wave-instructions per particle-step, non-transcendental ones at
-    ISSUE_MODEL["plain"] cycles each, transcendentals co-issued (free), over
-    the SIMD cycles the launch had per particle-step at its measured clock."""
+    instruction stream (the PMC pass's VALU and transcendental
+    wave-instructions per particle-step) against its calibrated issue floor
+    (issue_floor, ISSUE_MODEL at the sweep's waves per SIMD), over the SIMD
+    cycles the launch had per particle-step at its measured clock."""
     tf = mh_rate * f_alg / 1e12
     out = {"bound": "valu", "achieved": tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
            "frac": tf / FP32_PEAK_TFLOPS, "alg_flop_per_particle_step": f_alg,
@@ -575,30 +600,21 @@ def roofline_valu(args, mh_rate, f_alg, launch_steps, mh_ms):
         out["issue"] = {"omitted": src}
         return out
     try:
-        ps = d["per_particle_step"]
-        valu, trans = ps["SQ_INSTS_VALU"], ps.get("SQ_INSTS_VALU_TRANS_F32") or 0.0
         clk = (d.get("effective_clock") or {}).get("ghz") or 2.4
-        avail = 256 * 4 * clk * 1e9 * mh_ms * 1e-3 / launch_steps
-        floor = ISSUE_MODEL["plain"] * (valu - trans)
-        out["issue"] = {"valu_wave_insts_per_particle_step": valu,
-                        "trans_wave_insts_per_particle_step": trans,
-                        "floor_cycles_per_particle_step": floor,
-                        "available_cycles_per_particle_step": avail, "clock_ghz": clk,
-                        "issue_frac": floor / avail, "cycles_per_valu_inst": avail / valu,
-                        "model": ISSUE_MODEL, "source": src}
+        out["issue"] = dict(issue_floor(d["per_particle_step"], tile, clk, mh_ms, launch_steps),
+                            model=ISSUE_MODEL["floor"], probe=ISSUE_MODEL["probe"], source=src)
     except Exception as e:  # never fail the bench line on it
         out["issue"] = {"error": repr(e)}
     return out
 
 
-def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
+def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms, tile):
     """The binding resource (FP32 VALU issue).  reference_equivalent: SURVEY
     §8d's FLOPs of the reference's full re-render per particle-step, which the
-    incremental kernel does not execute (~15x fewer).  executed: from the
-    kernel's own VALU instruction counts (rocprofv3 PMC pass, profiles/
-    PMC_VALU_FILE, same workload): wave-instructions issued per second against
-    the issue peak of 256 CUs x 4 SIMDs x one wave-instruction per 4 cycles at
-    2.4 GHz, and the FP32 FLOPs they execute (64 lanes; FMA 2, packed x2)."""
+    incremental kernel does not execute.  executed: from the kernel's own VALU
+    instruction counts (rocprofv3 PMC pass, profiles/PMC_FILES, same
+    workload): the FP32 FLOPs they execute (64 lanes; FMA 2, packed x2) and
+    the stream against its calibrated issue floor (issue_floor)."""
     out = {"bound": "valu", "mh_particle_steps_per_s": mh_rate,
            "reference_equivalent": {
                "alg_flop_per_particle_step": f_alg,
@@ -607,53 +623,22 @@ def compute_block(args, mh_rate, f_alg, launch_steps, mh_ms):
     d, src = pmc_summary(args)
     if d is None:
         out["executed"] = {"omitted": src}
-    else:
-        try:
-            per_step = d["per_particle_step"]
-            insts = per_step["SQ_INSTS_VALU"] * launch_steps     # wave-instructions per launch
-            # SQ_INSTS_VALU_FLOPS_FP32(_TRANS) count FLOPs per wave-instruction
-            # (FMA 2, packed 2x): x 64 lanes
-            flops = 64 * per_step["fp32_flop"] * launch_steps
-            t = mh_ms * 1e-3
-            out["executed"] = {
-                "valu_wave_insts_per_particle_step": per_step["SQ_INSTS_VALU"],
-                "fp32_flop_per_particle_step": 64 * per_step["fp32_flop"],
-                "trans_wave_insts_per_particle_step": per_step.get("SQ_INSTS_VALU_TRANS_F32"),
-                "valu_issue_rate": insts / t, "valu_issue_peak": VALU_ISSUE_PEAK,
-                "valu_issue_frac": insts / t / VALU_ISSUE_PEAK,
-                "tflops": flops / t / 1e12, "frac": flops / t / 1e12 / FP32_PEAK_TFLOPS,
-                "source": src, "source_hash": d.get("source_hash")}
-            # the instruction mix weighted by its measured issue cost: SIMD
-            # cycles the launch's VALU stream needs per particle-step (a lower
-            # bound: packed ops, 6.0 cycles, are counted as plain ones) against
-            # the SIMD cycles the launch had per particle-step
-            trans = per_step.get("SQ_INSTS_VALU_TRANS_F32") or 0.0
-            cyc = (per_step["SQ_INSTS_VALU"] - trans) * ISSUE_CYC_VALU + trans * ISSUE_CYC_TRANS
-            avail = SIMD_CYCLES_PER_S * t / launch_steps
-            out["executed"]["issue_cycles_per_particle_step"] = cyc
-            out["executed"]["issue_cycles_available"] = avail
-            out["executed"]["issue_cycle_frac"] = cyc / avail
-            # the model-free figure: SIMD cycles the launch had per VALU
-            # wave-instruction it issued (one stream alone needs 4.2 for a
-            # plain op, 8.6 for a transcendental; many waves interleave below
-            # that -- near 4 the SIMDs issue VALU every slot they have)
-            out["executed"]["simd_cycles_per_valu_inst"] = avail / per_step["SQ_INSTS_VALU"]
-            # the same at the clock the launch actually ran at: GRBM_GUI_ACTIVE
-            # / 8 XCDs / the profiled launch's duration (MI355X_MICROARCH.md,
-            # "DVFS give-back"); the profiled pass's own cycles per particle-step
-            # need no clock at all
-            clk = d.get("effective_clock")
-            if clk:
-                ghz = clk["ghz"]
-                avail_eff = 256 * 4 * ghz * 1e9 * t / launch_steps
-                out["executed"]["effective_clock_ghz"] = ghz
-                out["executed"]["issue_cycles_available_at_effective_clock"] = avail_eff
-                out["executed"]["issue_cycle_frac_at_effective_clock"] = cyc / avail_eff
-                out["executed"]["issue_cycle_frac_profiled_launch"] = (
-                    cyc * launch_steps / (256 * 4 * clk["cycles_per_xcd"]))
-                out["executed"]["effective_clock_source"] = clk.get("note")
-        except Exception as e:  # never fail the bench line on it
-            out["executed"] = {"error": repr(e)}
+        return out
+    try:
+        per_step = d["per_particle_step"]
+        # SQ_INSTS_VALU_FLOPS_FP32(_TRANS) count FLOPs per wave-instruction
+        # (FMA 2, packed 2x): x 64 lanes
+        flops = 64 * per_step["fp32_flop"] * launch_steps
+        t = mh_ms * 1e-3
+        clk = d.get("effective_clock") or {}
+        out["executed"] = {
+            "fp32_flop_per_particle_step": 64 * per_step["fp32_flop"],
+            "tflops": flops / t / 1e12, "frac": flops / t / 1e12 / FP32_PEAK_TFLOPS,
+            "issue": issue_floor(per_step, tile, clk.get("ghz") or 2.4, mh_ms, launch_steps),
+            "effective_clock_source": clk.get("note"),
+            "source": src, "source_hash": d.get("source_hash")}
+    except Exception as e:  # never fail the bench line on it
+        out["executed"] = {"error": repr(e)}
     return out
 
 
@@ -894,7 +879,8 @@ def workload_leg(args, dev, rank, world, dist, backend, name):
                         "kernel_timing": f"HIP dispatch events, {len(ev)} launches"}}
     pmc, _ = pmc_summary(a2)
     out["roofline"]["traffic"] = pmc.get("hbm_bytes_per_launch") if pmc else None
-    out["compute"] = compute_block(a2, mh_rate, f_alg, steps_per_step, mh_ms)
+    out["roofline_valu"] = roofline_valu(a2, mh_rate, f_alg, steps_per_step, mh_ms, cfg["tile"])
+    out["compute"] = compute_block(a2, mh_rate, f_alg, steps_per_step, mh_ms, cfg["tile"])
     if name == "c3_rank_share":
         out["projected_8gpu_c3_value"] = 8 * out["value"]
         out["note"] = ("one rank's share (8 tiles) of the 64-tile C3 split at 8 GPUs, run on "
@@ -1198,8 +1184,8 @@ def main():
                                             "launches of the timed steps, replayed identically "
                                             "(step_attribution)"),
                      "alg_bytes_per_particle_step": b_alg},
-        "roofline_valu": roofline_valu(args, mh_rate, f_alg, launch_steps, mh_ms),
-        "compute": compute_block(args, mh_rate, f_alg, launch_steps, mh_ms),
+        "roofline_valu": roofline_valu(args, mh_rate, f_alg, launch_steps, mh_ms, cfg["tile"]),
+        "compute": compute_block(args, mh_rate, f_alg, launch_steps, mh_ms, cfg["tile"]),
         "smc": {"temperature_min": float(s.temperature.min()),
                 "acc_rate": float(s.mutation_acc_rates.mean()),
                 "ess_mean": float(s.ess.mean())},
