@@ -7,11 +7,14 @@ SRCS := $(CSRC)/common.hip $(CSRC)/model_kernels.hip $(CSRC)/mh_kernel.hip $(CSR
 HDRS := $(CSRC)/device.h $(CSRC)/render.h $(CSRC)/mcmc.h $(CSRC)/tile.h include/smcdet_hip.h
 OBJS := $(SRCS:.hip=.o)
 LIB := smcdet_amd/libsmcdet_hip.so
+DIAG_DIR := build/diag
+DIAG_LIB := smcdet_amd/libsmcdet_hip_diag.so
+DIAG_OBJS := $(patsubst $(CSRC)/%.hip,$(DIAG_DIR)/%.o,$(SRCS))
 # build provenance: sha1 of the sources in this order (smcdet_amd/_hip.py
 # SOURCES recomputes it and refuses a library built from other sources)
 SRC_HASH := $(shell cat $(SRCS) $(HDRS) | sha1sum | cut -c1-40)
 
-all: $(LIB) oracle
+all: $(LIB) $(DIAG_LIB) oracle
 
 $(CSRC)/%.o: $(CSRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -26,6 +29,20 @@ $(LIB): $(OBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# diagnostic build: the product's kernels plus the A/B and timing-only
+# variants (radial PSF table, scalar slots, ablations, no 1/v cache), which the
+# product library refuses; tests reach it through
+# smcdet_amd._hip.diag_library()
+diag: $(DIAG_LIB)
+$(DIAG_DIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	mkdir -p $(DIAG_DIR)
+	$(HIPCC) $(HIPFLAGS) -DSMCDET_DIAG -c $< -o $@
+$(DIAG_DIR)/common.o: $(SRCS) $(HDRS)
+	mkdir -p $(DIAG_DIR)
+	$(HIPCC) $(HIPFLAGS) -DSMCDET_DIAG -DSMCDET_SRC_HASH=\"$(SRC_HASH)\" -c $(CSRC)/common.hip -o $@
+$(DIAG_LIB): $(DIAG_OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(DIAG_OBJS)
+
 # profiling build with in-kernel phase timestamps (scripts/trace_phases.py)
 TRACE_LIB := smcdet_amd/libsmcdet_hip_trace.so
 trace: $(TRACE_LIB)
@@ -33,10 +50,10 @@ $(TRACE_LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -DSMCDET_TRACE -shared -o $@ $(SRCS)
 
 clean:
-	rm -f $(OBJS) $(LIB) $(TRACE_LIB)
+	rm -f $(OBJS) $(LIB) $(TRACE_LIB) $(DIAG_LIB) $(DIAG_OBJS)
 	$(MAKE) -C oracle clean
 
-.PHONY: all clean oracle trace
+.PHONY: all clean oracle trace diag
 
 # host sanitizer builds: the C oracle and the library's host side
 # (-Xarch_host -fsanitize=..., device code not compiled: nothing is launched)

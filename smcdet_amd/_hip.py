@@ -334,32 +334,74 @@ def built_hash(L=None):
     return v.rsplit("src ", 1)[-1] if "src " in v else None
 
 
+def _load(path):
+    """A checked _Lib over the library at `path` (signatures bound, sources
+    hash checked unless SMCDET_ALLOW_STALE=1)."""
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"smcdet_amd: HIP library not found at {path}; build it with `make` "
+            "(or __graft_entry__.build())")
+    L = ctypes.CDLL(path)
+    stale_ok = os.environ.get("SMCDET_ALLOW_STALE") == "1"
+    for name, (args, res) in _SIGS.items():
+        if stale_ok and not hasattr(L, name):
+            continue  # an older library in a same-box A/B (entry point absent)
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    if not stale_ok:
+        src, built = source_hash(), built_hash(L)
+        if src is not None and built != src:
+            raise RuntimeError(
+                f"smcdet_amd: {path} was built from sources with sha1 {built}, the "
+                f"sources here hash to {src}: rebuild with `make`")
+    return _Lib(L)
+
+
+# the diagnostic build (make diag): the product's kernels plus the A/B and
+# timing-only MH variants the product refuses (PSF table, scalar slots,
+# ablations, no 1/v cache); reached only inside diag_library()
+DIAG_LIB_PATH = os.path.join(_HERE, "libsmcdet_hip_diag.so")
+_diag = None
+_override = threading.local()
+
+
 def lib():
     """Load libsmcdet_hip.so once.  Raises if it is missing (there is no
     fallback) or if it was built from other sources than the ones next to it
-    (a stale library; SMCDET_ALLOW_STALE=1 skips that check)."""
+    (a stale library; SMCDET_ALLOW_STALE=1 skips that check).  Inside
+    diag_library() (this thread): the diagnostic build instead."""
     global _lib
+    o = getattr(_override, "lib", None)
+    if o is not None:
+        return o
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(
-                f"smcdet_amd: HIP library not found at {LIB_PATH}; build it with `make` "
-                "(or __graft_entry__.build())")
-        L = ctypes.CDLL(LIB_PATH)
-        stale_ok = os.environ.get("SMCDET_ALLOW_STALE") == "1"
-        for name, (args, res) in _SIGS.items():
-            if stale_ok and not hasattr(L, name):
-                continue  # an older library in a same-box A/B (entry point absent)
-            fn = getattr(L, name)
-            fn.argtypes = args
-            fn.restype = res
-        if not stale_ok:
-            src, built = source_hash(), built_hash(L)
-            if src is not None and built != src:
-                raise RuntimeError(
-                    f"smcdet_amd: {LIB_PATH} was built from sources with sha1 {built}, the "
-                    f"sources here hash to {src}: rebuild with `make`")
-        _lib = _Lib(L)
+        _lib = _load(LIB_PATH)
     return _lib
+
+
+def is_diag(L=None) -> bool:
+    return ", diag)" in (L or lib()).smcdet_version().decode()
+
+
+class diag_library:
+    """Context manager: library calls of this thread go to the diagnostic
+    build (tests of the A/B variants against the product's kernels; the
+    product library refuses their flags).  Raises if it is not built."""
+
+    def __enter__(self):
+        global _diag
+        if _diag is None:
+            _diag = _load(DIAG_LIB_PATH)
+            if not is_diag(_diag):
+                raise RuntimeError(f"{DIAG_LIB_PATH} is not a diagnostic build")
+        self._prev = getattr(_override, "lib", None)
+        _override.lib = _diag
+        return _diag
+
+    def __exit__(self, *exc):
+        _override.lib = self._prev
+        return False
 
 
 def version() -> str:

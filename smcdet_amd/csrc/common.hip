@@ -198,7 +198,15 @@ int smcdet_launch_timing_tiles(int32_t on) {
 #define SMCDET_SRC_HASH "unknown"
 #endif
 // "src <sha1>": the sha1 of the library's sources (Makefile SRC_HASH)
-const char* smcdet_version(void) { return "smcdet_hip 0.2.0 (gfx950) src " SMCDET_SRC_HASH; }
+// the diagnostic build (make diag) says so: "(gfx950, diag)"
+#ifdef SMCDET_DIAG
+#define SMCDET_BUILD_KIND ", diag"
+#else
+#define SMCDET_BUILD_KIND ""
+#endif
+const char* smcdet_version(void) {
+  return "smcdet_hip 0.2.0 (gfx950" SMCDET_BUILD_KIND ") src " SMCDET_SRC_HASH;
+}
 int32_t smcdet_abi_version(void) { return SMCDET_ABI_VERSION; }
 const char* smcdet_last_error(void) { return smcdet::g_err; }
 

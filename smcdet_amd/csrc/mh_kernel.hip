@@ -48,6 +48,19 @@ namespace smcdet {
 
 SMCDET_WAVE_TABLE
 
+// The diagnostic build (make diag -> libsmcdet_hip_diag.so, -DSMCDET_DIAG)
+// adds the A/B and timing-only variants: the radial PSF table
+// (SMCDET_MH_PSF_TABLE), scalar union-window slots (SMCDET_MH_SCALAR_SLOTS),
+// the ablations (SMCDET_MH_ABLATE_*), the sweep without the 1/v cache
+// (SMCDET_MH_NO_RCP_CACHE) and the SMCDET_MH_BLOCK_SLOTS override.  The product
+// library compiles only the instantiations its API paths dispatch and refuses
+// those flags (instantiation table).
+#ifdef SMCDET_DIAG
+constexpr bool kDiag = true;
+#else
+constexpr bool kDiag = false;
+#endif
+
 constexpr int kMhWaves = 4;
 constexpr int kMhBlock = kMhWaves * kWave;
 constexpr int kSlots = 6;  // register-resident window passes (6*64 = 384 positions)
@@ -415,8 +428,16 @@ __device__ __forceinline__ void copy_out_regs(const float* lam, float* __restric
 #ifndef SMCDET_SMALL_TILE_WAVES
 #define SMCDET_SMALL_TILE_WAVES 7
 #endif
-template <int PPL>
-constexpr int mh_waves_per_eu() { return PPL == 1 ? SMCDET_SMALL_TILE_WAVES : 4; }
+// (the replay instantiation of small tiles, tests only, holds the replayed
+// draws too: 6 waves per SIMD, 80 VGPRs, instead of spilling at 72; FULL
+// mode's register re-render of 65..1024-pixel tiles -- the reference's
+// arithmetic, a parity control, bit-identical to the loglik kernel's render --
+// runs at 2 waves per SIMD instead of spilling at 128 VGPRs)
+template <int PPL, bool REPLAY = false, bool FULL = false>
+constexpr int mh_waves_per_eu() {
+  return PPL == 1 ? (REPLAY ? SMCDET_SMALL_TILE_WAVES - 1 : SMCDET_SMALL_TILE_WAVES)
+                  : (FULL && PPL == 16 ? 2 : 4);
+}
 template <int PPL>
 constexpr int mh_slots() { return PPL == 1 ? 1 : kSlots; }
 
@@ -438,7 +459,8 @@ constexpr int mh_slots() { return PPL == 1 ? 1 : kSlots; }
 // (and the PSF cache's rows) comes from the table.
 template <int MODEL, bool REPLAY, bool FULL, int PPL, bool PAIRED, bool TAIL, bool GL = false,
           bool PC = false, bool RV = false, bool TB = false>
-__global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_kernel(MhArgs a) {
+__global__ __launch_bounds__(kMhBlock, (mh_waves_per_eu<PPL, REPLAY, FULL>())) void mh_sweep_kernel(
+    MhArgs a) {
   static_assert(!PC || (PPL == 1 && !FULL && !GL && !TAIL), "PSF cache: small incremental tiles");
   static_assert(!RV || (MODEL == SMCDET_MODEL_M71 && PPL > 1 && !FULL && !GL && !TAIL && PAIRED),
                 "1/v cache: M71 register-render tiles, incremental, paired");
@@ -634,8 +656,8 @@ __global__ __launch_bounds__(kMhBlock, mh_waves_per_eu<PPL>()) void mh_sweep_ker
     dm.lb = d == 0 ? lb_h : (d == 1 ? lb_w : a.lb_f);
     dm.ub = d == 0 ? ub_h : (d == 1 ? ub_w : a.ub_f);
   }
-  const bool ablate_prop = (a.ablate & SMCDET_MH_ABLATE_PROPOSAL) != 0;
-  const bool ablate_lik = (a.ablate & SMCDET_MH_ABLATE_LIKELIHOOD) != 0;
+  const bool ablate_prop = kDiag && (a.ablate & SMCDET_MH_ABLATE_PROPOSAL) != 0;
+  const bool ablate_lik = kDiag && (a.ablate & SMCDET_MH_ABLATE_LIKELIHOOD) != 0;
 
   // ---- draws: lane i of the cache holds iteration (block*64 + i) ------------
   float ru0 = 0.f, ru1 = 0.f, ru2 = 0.f, ru3 = 0.f, ru4 = 0.f;
@@ -1227,7 +1249,8 @@ template <int MODEL, bool REPLAY, bool FULL, int PPL>
 static int launch_mh1(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
   // FULL mode never evaluates union-window slots: one instantiation
   constexpr bool kPair = !FULL;
-  const bool paired = kPair && !a.scalar_slots;
+  // (scalar slots: diagnostic build only, host-checked)
+  const bool paired = kPair && !(kDiag && a.scalar_slots);
   // the fused tail exists only where tail_fusable() allows it
   constexpr bool kTail = !FULL && PPL != 1;
   const bool tail = kTail && paired && a.has_tail;
@@ -1235,12 +1258,12 @@ static int launch_mh1(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
   // The LDS-cached variants, richest first, where their workgroups per CU
   // (the occupancy the instantiation is built for) still fit the 160 KiB:
   // PC (small tiles) = the per-wave PSF cache, RV (M71, 65..1024 px) = the
-  // per-wave 1/v image, TB = the radial PSF table (a.psf_tab set by the host
-  // for M71 models whose table passes its accuracy check).
+  // per-wave 1/v image, TB = the radial PSF table (diagnostic build: a.psf_tab
+  // set by the host for M71 models whose table passes its accuracy check).
   auto fits = [&](size_t bytes, int wg_per_cu) {
     return (size_t)wg_per_cu * (bytes + 1024) <= 160 * 1024;
   };
-  auto with_tab = [&](size_t bytes) {
+  [[maybe_unused]] auto with_tab = [&](size_t bytes) {
     return ((bytes + 15) & ~(size_t)15) + (size_t)kTabNodes * sizeof(float4);
   };
   auto go_variant = [&](auto kern, size_t bytes) -> int {
@@ -1249,12 +1272,12 @@ static int launch_mh1(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
     launch_sweep(kern, grid, dim3(kMhBlock), bytes, st, a);
     return SMCDET_OK;
   };
-  const bool tb = a.psf_tab != nullptr && paired && !tail;
+  [[maybe_unused]] const bool tb = kDiag && a.psf_tab != nullptr && paired && !tail;
   if constexpr (PPL == 1 && !FULL) {
     // small tiles: the PSF cache (S rows of H*W floats per wave)
     const size_t lds_pc = lds + (size_t)kMhWaves * a.S * a.m.H * a.m.W * sizeof(float);
     constexpr int wg = SMCDET_SMALL_TILE_WAVES;
-    if constexpr (MODEL == SMCDET_MODEL_M71) {
+    if constexpr (MODEL == SMCDET_MODEL_M71 && kDiag) {
       if (tb && !a.no_psf_cache && fits(with_tab(lds_pc), wg))
         return go_variant(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, true,
                                           false, true>, with_tab(lds_pc));
@@ -1262,7 +1285,7 @@ static int launch_mh1(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
     if (paired && !a.no_psf_cache && fits(lds_pc, wg))
       return go_variant(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, true>,
                         lds_pc);
-    if constexpr (MODEL == SMCDET_MODEL_M71) {
+    if constexpr (MODEL == SMCDET_MODEL_M71 && kDiag) {
       if (tb && fits(with_tab(lds), wg))
         return go_variant(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, false,
                                           false, true>, with_tab(lds));
@@ -1270,30 +1293,55 @@ static int launch_mh1(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
   }
   if constexpr (MODEL == SMCDET_MODEL_M71 && PPL > 1 && !FULL) {
     // M71 register-render tiles: the 1/v image (HWp floats per wave) and / or
-    // the PSF table, at 4 workgroups per CU (4 waves per SIMD)
+    // the PSF table, at 4 workgroups per CU (4 waves per SIMD).  The 1/v image
+    // always fits at these sizes (9 (H*W + 64) floats per workgroup), so
+    // the product's only other M71 variant here is the fused tail's.
     const size_t lds_rv = lds + (size_t)kMhWaves * (a.m.H * a.m.W + kWave) * sizeof(float);
-    const bool rv = paired && !tail && !a.no_rcp_cache;
-    if (tb && rv && fits(with_tab(lds_rv), 4))
-      return go_variant(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, false, true,
-                                        true>, with_tab(lds_rv));
-    if (tb && fits(with_tab(lds), 4))
-      return go_variant(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, false,
-                                        false, true>, with_tab(lds));
+    const bool rv = paired && !tail && !(kDiag && a.no_rcp_cache);
+    if constexpr (kDiag) {
+      if (tb && rv && fits(with_tab(lds_rv), 4))
+        return go_variant(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, false,
+                                          true, true>, with_tab(lds_rv));
+      if (tb && fits(with_tab(lds), 4))
+        return go_variant(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, false,
+                                          false, true>, with_tab(lds));
+    }
     if (rv && fits(lds_rv, 4))
       return go_variant(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, true, false, false, false, true>,
                         lds_rv);
+    if constexpr (!kDiag) {
+      if (!tail) return set_error(SMCDET_EUNSUPPORTED, "M71 sweep: the 1/v image does not fit");
+    }
   }
-  const void* fn = tail     ?(const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, kTail>
-                   : paired ? (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, false>
-                            : (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, false, false>;
+  // M71 register-render tiles without the fused tail take the 1/v variant
+  // above: the plain paired instantiation is the diagnostic build's
+  // (SMCDET_MH_NO_RCP_CACHE) there; scalar slots likewise
+  constexpr bool kPlainPaired = kPair && (kDiag || !(MODEL == SMCDET_MODEL_M71 && PPL > 1));
+  constexpr bool kUnpaired = FULL || kDiag;
+  const void* fn = nullptr;
+  if (tail) {
+    if constexpr (kTail) fn = (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, kTail>;
+  } else if (paired) {
+    if constexpr (kPlainPaired) fn = (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, false>;
+  } else {
+    if constexpr (kUnpaired) fn = (const void*)mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, false, false>;
+  }
+  if (!fn) return set_error(SMCDET_EUNSUPPORTED, "MH sweep variant not in this build");
   int rc = ensure_lds(fn, lds);
   if (rc) return rc;
-  if (tail)
-    launch_sweep(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, kTail>, grid, dim3(kMhBlock), lds, st, a);
-  else if (paired)
-    launch_sweep(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, false>, grid, dim3(kMhBlock), lds, st, a);
-  else
-    launch_sweep(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, false, false>, grid, dim3(kMhBlock), lds, st, a);
+  if (tail) {
+    if constexpr (kTail)
+      launch_sweep(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, kTail>, grid, dim3(kMhBlock),
+                   lds, st, a);
+  } else if (paired) {
+    if constexpr (kPlainPaired)
+      launch_sweep(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, kPair, false>, grid, dim3(kMhBlock),
+                   lds, st, a);
+  } else {
+    if constexpr (kUnpaired)
+      launch_sweep(mh_sweep_kernel<MODEL, REPLAY, FULL, PPL, false, false>, grid, dim3(kMhBlock),
+                   lds, st, a);
+  }
   return SMCDET_OK;
 }
 
@@ -1301,7 +1349,7 @@ static int launch_mh1(const MhArgs& a, dim3 grid, size_t lds, hipStream_t st) {
 // fused tail, no dynamic LDS
 template <int MODEL, bool REPLAY, bool FULL>
 static int launch_mh_gl(const MhArgs& a, dim3 grid, hipStream_t st) {
-  if (a.has_tail || a.scalar_slots)
+  if (a.has_tail || (kDiag && a.scalar_slots))
     return set_error(SMCDET_EUNSUPPORTED, "tiles above %d pixels: no fused step / scalar slots",
                      kMaxLdsPixels);
   constexpr bool kPair = !FULL;
@@ -1357,6 +1405,7 @@ static bool tail_fusable(const smcdet_image_model_t& m, int N, int S, uint32_t f
   return 4 * (need + 2048) <= 160 * 1024;
 }
 
+#ifdef SMCDET_DIAG  // the radial PSF table: diagnostic build only
 // ---- the radial PSF table (psf_tab, device.h) --------------------------------
 // Device copies live in a module-scope table of slots, one per (device, PSF
 // parameters); a slot is filled once (upload + stream synchronisation, so any
@@ -1490,6 +1539,7 @@ static int psf_table_device(const smcdet_image_model_t& mdl, const DevModel& m, 
   return SMCDET_OK;
 }
 }  // namespace smcdet
+#endif  // SMCDET_DIAG
 
 static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t* prior,
                          const smcdet_mh_t* mh, const float* tiled_image,
@@ -1641,6 +1691,12 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
     }
   }
   const bool full = (flags & SMCDET_MH_FULL_RECOMPUTE) != 0;
+  if (!kDiag && (flags & (SMCDET_MH_ABLATE_LIKELIHOOD | SMCDET_MH_ABLATE_PROPOSAL |
+                          SMCDET_MH_SCALAR_SLOTS | SMCDET_MH_PSF_TABLE | SMCDET_MH_NO_RCP_CACHE)))
+    return set_error(SMCDET_EUNSUPPORTED,
+                     "MH flags 0x%x: diagnostic variants (ablations, scalar slots, PSF table, no "
+                     "1/v cache) are in the diagnostic build only (make diag -> "
+                     "libsmcdet_hip_diag.so)", flags);
   a.ablate = flags & (SMCDET_MH_ABLATE_LIKELIHOOD | SMCDET_MH_ABLATE_PROPOSAL);
   a.by_count = (flags & SMCDET_MH_COMPONENT_BY_COUNT) != 0;
   a.scalar_slots = (flags & SMCDET_MH_SCALAR_SLOTS) != 0;
@@ -1655,10 +1711,12 @@ static int mh_sweep_impl(const smcdet_image_model_t* model, const smcdet_prior_t
   // product never reads the environment on the launch path)
   if (const char* e = getenv("SMCDET_MH_BLOCK_SLOTS")) a.blk_slots = atoi(e);
 #endif
-  if (a.m.model == SMCDET_MODEL_M71 && !full && !global_tile && !a.scalar_slots &&
+  if (kDiag && a.m.model == SMCDET_MODEL_M71 && !full && !global_tile && !a.scalar_slots &&
       (flags & SMCDET_MH_PSF_TABLE)) {
+#ifdef SMCDET_DIAG
     rc = psf_table_device(*model, a.m, st, &a.psf_tab, &a.tab_inv_h);
     if (rc) return rc;
+#endif
   }
   rc = a.m.model == SMCDET_MODEL_M71
            ? launch_mh<SMCDET_MODEL_M71>(a, replay != nullptr, full, grid, lds, st)

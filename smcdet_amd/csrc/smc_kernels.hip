@@ -28,12 +28,18 @@ __global__ __launch_bounds__(NT) void tile_kernel(TileArgs a) {
   tile_work<NT, PER>(a, t, buf, red, threadIdx.x < kWave ? t : -1);
 }
 
+// 512 threads; the 256-thread tile kernel (measured slower)
+// is the diagnostic build's A/B (SMCDET_TILE_THREADS=256)
 static int tile_threads() {
+#ifdef SMCDET_DIAG
   static const int nt = [] {
     const char* e = getenv("SMCDET_TILE_THREADS");
     return (e && atoi(e) == 256) ? 256 : 512;
   }();
   return nt;
+#else
+  return 512;
+#endif
 }
 
 // gather: thread per (t, n, s)
@@ -347,8 +353,13 @@ int launch_tile(const TileArgs& a, hipStream_t st) {
          : per <= 16 ? (const void*)tile_kernel<n, 16>
                      : (const void*)tile_kernel<n, 32>;
   };
+#ifdef SMCDET_DIAG
   const void* fn = nt == 256 ? pick(std::integral_constant<int, 256>{})
                              : pick(std::integral_constant<int, 512>{});
+#else
+  (void)nt;
+  const void* fn = pick(std::integral_constant<int, 512>{});
+#endif
   int rc = ensure_lds(fn, lds + sizeof(TileRed));
   if (rc) return rc;
   void* args[] = {const_cast<TileArgs*>(&a)};

@@ -199,3 +199,48 @@ def test_checked_wrapper_forwards_argtypes():
     w.restype = ctypes.c_size_t
     assert raw.argtypes == [ctypes.c_char_p] and raw.restype is ctypes.c_size_t
     assert w(b"graft") == 5
+
+
+def _mh_call(L, flags):
+    """smcdet_mh_sweep with valid descriptors and placeholder device pointers
+    (never dereferenced: the calls below stop at argument validation, or at
+    the launch on a machine without a GPU)."""
+    m = _hip.ImageModelC()
+    m.model, m.H, m.W, m.psf_radius = 1, 32, 32, 8
+    m.background, m.adu_per_nmgy, m.psf_norm = 100.0, 1.0, 1.0
+    m.psf_params[:] = [1.0, 2.0, 2.0, 5.0, 0.5, 0.5]
+    m.noise_additive, m.noise_multiplicative = 1e-10, 1.9
+    p = _hip.PriorC()
+    p.kind, p.min_objects, p.max_objects = 1, 10, 10
+    p.loc_low, p.loc_high_h, p.loc_high_w = -4.0, 36.0, 36.0
+    p.poisson_mean, p.flux_alpha, p.flux_lower, p.flux_upper = 5.0, 0.2, 0.06, 1800.0
+    mh = _hip.MHC()
+    mh.num_iters, mh.locs_stdev, mh.fluxes_stdev = 1, 0.1, 2.5
+    mh.fluxes_min, mh.fluxes_max = 0.06, 1800.0
+    mh.locs_min_h = mh.locs_min_w = -4.0
+    mh.locs_max_h = mh.locs_max_w = 36.0
+    P = [ctypes.c_void_p(0x100000 * (i + 1)) for i in range(16)]
+    return L.smcdet_mh_sweep(ctypes.byref(m), ctypes.byref(p), ctypes.byref(mh), P[0], P[1],
+                             1, 64, 10, None, P[2], P[3], P[4], P[5], P[6], P[7], None, None,
+                             1, 0, None, flags, P[8], P[9], P[10], None, None, None)
+
+
+def test_product_refuses_diagnostic_flags_and_diag_build_takes_them():
+    """The product library compiles only the dispatched MH variants and refuses
+    the diagnostic ones (ablations 256/512, scalar slots 1024, PSF table 8192,
+    no 1/v cache 4096: include/smcdet_hip.h) before any device work; the
+    diagnostic build (make diag) gets past that check."""
+    L = _hip.lib()
+    assert not _hip.is_diag(L)
+    for flag in (256, 512, 1024, 4096, 8192):
+        rc = _mh_call(L, flag)
+        assert rc == -2, (flag, rc)
+        assert b"diagnostic build" in L.smcdet_last_error(), flag
+    if not os.path.exists(_hip.DIAG_LIB_PATH):
+        pytest.skip("diagnostic build not made")
+    with _hip.diag_library() as D:
+        assert _hip.lib() is D and _hip.is_diag(D)
+        for flag in (256, 1024, 4096):
+            _mh_call(D, flag)
+            assert b"diagnostic build" not in D.smcdet_last_error(), flag
+    assert _hip.lib() is L

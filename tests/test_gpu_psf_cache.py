@@ -8,6 +8,8 @@ parity with the reference is pinned by the 8x8 replays of
 test_gpu_parity.py (mh_m71_8x8, mh_m71_edge_8x8, mh_m71_tiles and the
 recorded SMC runs), which now run through it.
 """
+import contextlib
+
 import numpy as np
 import pytest
 import torch
@@ -19,6 +21,16 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 NO_PSF_CACHE = 2048  # include/smcdet_hip.h
 PSF_TABLE = 8192
+NO_RCP_CACHE = 4096
+DIAG_FLAGS = PSF_TABLE | NO_RCP_CACHE
+
+
+def _lib_for(flags):
+    """The library a variant lives in: the product's own kernels, or -- for the
+    diagnostic variants (PSF table, no 1/v cache), which the product refuses --
+    the diagnostic build (make diag), in the same process."""
+    from smcdet_amd import _hip
+    return _hip.diag_library() if flags & DIAG_FLAGS else contextlib.nullcontext()
 
 
 def _m71_image(H, seed, n_tiles, counts_rate=0.004):
@@ -34,8 +46,9 @@ def _run(img, td, prior, model, mh, N, seed, cache, by_count=False, flags=0):
     s = SMCsampler(img, td, prior, model, mh, N, 0.5, "systematic",
                    M71["flux_detection_threshold"], 200, print_every=10 ** 9, seed=seed,
                    device=DEV)
-    s.run()
-    torch.cuda.synchronize()
+    with _lib_for(flags):
+        s.run()
+        torch.cuda.synchronize()
     return {k: getattr(s, k).detach().cpu().numpy().copy()
             for k in ("temperature", "log_normalizing_constant", "ess", "locs", "fluxes",
                       "counts", "loglik", "mutation_acc_rates")} | {"iter": np.array(s.iter)}
@@ -73,9 +86,6 @@ def test_psf_cache_poisson_8x8_run_is_bit_identical():
     _assert_same(*out)
 
 
-NO_RCP_CACHE = 4096  # include/smcdet_hip.h
-
-
 @pytest.mark.parametrize("H,N,base", [(32, 1024, 0), (16, 512, 0), (16, 512, PSF_TABLE)])
 def test_rcp_cache_m71_run_is_bit_identical(H, N, base):
     """M71 tiles of 65..1024 pixels keep a per-wave image of 1/(s0^2 + eta*rate)
@@ -83,7 +93,9 @@ def test_rcp_cache_m71_run_is_bit_identical(H, N, base):
     own reciprocal of the new rate is stored): whole C2-geometry runs are
     bit-identical with and without it (SMCDET_MH_NO_RCP_CACHE); 16x16 tiles
     also with the opt-in PSF table (SMCDET_MH_PSF_TABLE), which at 32x32 takes
-    the LDS the 1/v image needs."""
+    the LDS the 1/v image needs.  The sweeps without the 1/v image (and the
+    table's) are the diagnostic build's: base 0 compares the PRODUCT library's
+    sweep with the diagnostic build's uncached one."""
     img = _m71_image(H, 31 + H, 1)
     out = []
     for flags in (base, base | NO_RCP_CACHE):
@@ -93,8 +105,9 @@ def test_rcp_cache_m71_run_is_bit_identical(H, N, base):
         s = SMCsampler(img, H, p_m71_prior(H, 10, 10, counts_rate=0.003125), p_m71_model(H), mh,
                        N, 0.5, "systematic", M71["flux_detection_threshold"], 200,
                        print_every=10 ** 9, seed=13, device=DEV)
-        s.run()
-        torch.cuda.synchronize()
+        with _lib_for(flags):
+            s.run()
+            torch.cuda.synchronize()
         out.append({k: getattr(s, k).detach().cpu().numpy().copy()
                      for k in ("temperature", "log_normalizing_constant", "ess", "locs", "fluxes",
                                "loglik", "mutation_acc_rates")} | {"iter": np.array(s.iter)})
@@ -108,7 +121,7 @@ def test_psf_table_sweep_close_to_exp2_sweep():
     with the same Philox draws: the table's PSF values differ by float32
     rounding (<= 3e-7 relative), so the two sweeps make the same decisions
     except at near ties -- and they are not bit-identical (the table path
-    ran)."""
+    ran; the table is the diagnostic build's, the exp2 form the product's)."""
     from smcdet_amd._rng import PhiloxStream
     H, N, K = 32, 2048, 100
     img = _m71_image(H, 77, 1, counts_rate=0.003125)[None, None].contiguous()
@@ -122,7 +135,9 @@ def test_psf_table_sweep_close_to_exp2_sweep():
         mh = p_m71_mh(K)
         mh.debug_flags = flags
         mh.rng = PhiloxStream(17)
-        lo, fo, _ = mh.run(img, counts, locs, fluxes, tau, prior=prior, image_model=model)
+        with _lib_for(flags):
+            lo, fo, _ = mh.run(img, counts, locs, fluxes, tau, prior=prior, image_model=model)
+            torch.cuda.synchronize()
         res.append((lo.cpu().numpy(), fo.cpu().numpy(), mh.last_loglik.cpu().numpy()))
     same = np.all(res[0][0] == res[1][0], axis=(-1, -2)) & np.all(res[0][1] == res[1][1], axis=-1)
     assert same.mean() > 0.97, same.mean()
