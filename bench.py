@@ -53,9 +53,9 @@ F_ALG_PER_STEP = 68.0e3     # SURVEY §8d, S=10, 32x32
 # rocprofv3 PMC summary of the C2 MH launch (scripts/profile.sh + scripts/pmc_summary.py):
 # FETCH_SIZE / WRITE_SIZE (HBM traffic), SQ VALU counts, GRBM_GUI_ACTIVE (effective clock),
 # and the sha1 of the library sources it was measured on
-PMC_FILE = "pmc_mh_r05.json"
+PMC_FILE = "pmc_mh_r06.json"
 # the same for the C4 / C5 MH launches (the default run's `c4` / `c5` legs)
-PMC_FILES = {"c2": PMC_FILE, "c4": "pmc_mh_c4_r05.json", "c5": "pmc_mh_c5_r05.json"}
+PMC_FILES = {"c2": PMC_FILE, "c4": "pmc_mh_c4_r06.json", "c5": "pmc_mh_c5_r06.json"}
 # The VALU issue costs on gfx950, measured at the MH sweeps' occupancies
 # (scripts/probe/issue_probe.hip: per-SIMD s_memtime spans of 16 independent
 # chains per wave, profiles/r06/issue_probe.txt): SIMD cycles per
