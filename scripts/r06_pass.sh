@@ -48,6 +48,19 @@ if has profile; then
   tr=$(find $D/prof/trace -name 'run_kernel_trace.csv' | head -1)
   [ -n "$tr" ] && python scripts/step_attribution.py "$tr" --json $D/step_attribution.json | tail -8
 fi
+if has trace; then
+  # the bench line's own command (prewarm on) under a kernel trace: the last
+  # 20 steps' launches are the timed steps' identical replay, whose sweep /
+  # tile durations the line reports as step_attribution -- the two must agree
+  mkdir -p $D/trace_bench
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -T -f csv -d $D/trace_bench -o run -- \
+    python3 bench.py --no-c3 --no-legs --no-vs-ref --no-full-run --no-cpu-baseline --no-spread \
+    > $D/trace_bench.log 2>&1
+  step trace $?
+  tr=$(find $D/trace_bench -name 'run_kernel_trace.csv' | head -1)
+  [ -n "$tr" ] && python scripts/step_attribution.py "$tr" --tail 20 --json $D/trace_bench_attribution.json | tail -12
+  grep '^{' $D/trace_bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('bench line:', json.dumps({k: d['step_attribution'][k] for k in ('sweep_ms', 'tile_pass_ms', 'timed_ms_per_step')}))"
+fi
 if has c4pmc; then
   OUT=$D/prof_c4 BENCH_ARGS="--workload c4" SQ="$SQSET" SQ2="$SQ2SET" SQ3="$SQ3SET" \
     PSTEPS=10 bash scripts/profile.sh
