@@ -80,19 +80,22 @@ extern "C" {
  * and back-to-back launches on one stream leave no gap to recover
  * (DESIGN.md §4.2). */
 #define SMCDET_SMC_TWO_LAUNCH 2u
-/* diagnostic ablations (timing only; results are NOT valid samples) */
+/* Flags marked "diagnostic build only" are compiled into
+ * libsmcdet_hip_diag.so (make diag, -DSMCDET_DIAG) alone: the product library
+ * returns SMCDET_EUNSUPPORTED for them before any device work.
+ * diagnostic build only: ablations (timing only; results are NOT valid samples) */
 #define SMCDET_MH_ABLATE_LIKELIHOOD 256u /* skip the delta-likelihood passes */
 #define SMCDET_MH_ABLATE_PROPOSAL 512u   /* skip the truncated-normal proposal math */
-/* diagnostic: evaluate the union window one position per lane instead of two
+/* diagnostic build only: evaluate the union window one position per lane instead of two
  * (packed arithmetic); same results up to float32 summation order */
 #define SMCDET_MH_SCALAR_SLOTS 1024u
 /* diagnostic: small tiles (H*W <= 64) without the per-wave PSF cache (the
  * moved source's old PSF re-evaluated each iteration); same results */
 #define SMCDET_MH_NO_PSF_CACHE 2048u
-/* diagnostic: M71 tiles of 65..1024 pixels without the per-wave 1/v image
+/* diagnostic build only: M71 tiles of 65..1024 pixels without the per-wave 1/v image
  * (each pixel's 1/(s0^2 + eta*rate) formed per use); same results */
 #define SMCDET_MH_NO_RCP_CACHE 4096u
-/* diagnostic: M71 sweeps with the radial PSF table in LDS (the union
+/* diagnostic build only: M71 sweeps with the radial PSF table in LDS (the union
  * window's PSF values from a cubic table instead of exp2/log2; results differ
  * by float32 rounding of the profile, ~3e-7 relative).  Measured slower at
  * 32x32 (its LDS reads) and even at 8x8, so off by default */
