@@ -55,7 +55,8 @@ from tests._params import GOLDEN, M71, p_m71_mh, p_m71_model, p_m71_prior
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 TARGET = "stats_c2_moderate_4096_k100_oracle.json"
-CHUNKS = 4
+# (SMCDET_PAIRED_CHUNKS: more, shorter tests when every oracle run is replayed)
+CHUNKS = int(os.environ.get("SMCDET_PAIRED_CHUNKS", "4"))
 _results = {}
 
 
