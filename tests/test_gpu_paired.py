@@ -117,9 +117,12 @@ def paired_gpu_run(img, cfg, seed, full_recompute=False):
 def test_paired_runs_chunk(chunk):
     ref = _target()
     runs = ref["runs"]
+    # SMCDET_PAIRED_NO_TWIN=1 (the every-run replays): no full-recompute control
+    twin = os.environ.get("SMCDET_PAIRED_NO_TWIN") != "1"
     for r in runs[chunk::CHUNKS]:
         out = paired_gpu_run(ref["image"], ref["config"], r["seed"])
-        full = paired_gpu_run(ref["image"], ref["config"], r["seed"], full_recompute=True)
+        full = (paired_gpu_run(ref["image"], ref["config"], r["seed"], full_recompute=True)
+                if twin else {"logZ": float("nan"), "iters": -1})
         out["full_logZ"], out["full_iters"] = full["logZ"], full["iters"]
         out["oracle_logZ"], out["oracle_iters"] = r["logZ"], r["iters"]
         ot, gt = r["tau_trace"], out["tau"]
@@ -162,9 +165,10 @@ def test_paired_runs_same_mode():
     cut = float(np.median(lz_o) - 40.0)
     res = [_results[r["seed"]] for r in runs]
     gpu = _compare(np.array([x["logZ"] for x in res]), lz_o, cut)
-    full = _compare(np.array([x["full_logZ"] for x in res]), lz_o, cut)
+    has_twin = all(np.isfinite(x["full_logZ"]) for x in res)
+    full = _compare(np.array([x["full_logZ"] for x in res]), lz_o, cut) if has_twin else None
     twins = _compare(np.array([x["logZ"] for x in res]), np.array([x["full_logZ"] for x in res]),
-                     cut)
+                     cut) if has_twin else None
     first = np.array([x["first_tau_divergence"] for x in res])
     summary = dict(cut=cut, n=len(res), gpu_vs_oracle=gpu, full_recompute_vs_oracle=full,
                    gpu_vs_full_recompute=twins,
