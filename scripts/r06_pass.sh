@@ -35,6 +35,22 @@ if has probe; then
   step probe $?
   cat $D/issue_probe.txt
 fi
+if has law; then
+  # north_star's "log Z and ESS within 1%" by sample size (scripts/c2_law.py)
+  timeout -k 10 600 python -u scripts/c2_law.py ${LAW_RUNS:-8192} > $D/c2_law.json 2> $D/c2_law.err
+  step law $?
+  python -c "import json; d=json.load(open('$D/c2_law.json')); print({n: {k: (round(d[n][k]['rel_diff'], 5), [round(x, 5) for x in d[n][k]['rel_diff_95']]) for k in ('logZ', 'final_ess', 'iters')} for n in ('vs_oracle', 'vs_reference')})"
+fi
+if has paired; then
+  # every oracle run of the C2 target replayed on the GPU (tests/test_gpu_paired.py);
+  # -s: every seed's line reaches the log as it is written
+  SMCDET_PAIRED_ALL=1 SMCDET_PAIRED_NO_TWIN=${NO_TWIN:-1} SMCDET_PAIRED_CHUNKS=${CHUNKS:-48} \
+    SMCDET_PAIRED_OUT=$D/paired_all.json timeout -k 10 ${PAIRED_LIMIT:-3000} \
+    python -u -m pytest tests/test_gpu_paired.py -s -q -p no:cacheprovider --timeout 600 \
+    --timeout-method thread > $D/paired_all.log 2>&1
+  step paired $?
+  tail -4 $D/paired_all.log
+fi
 if has bench; then
   timeout -k 10 400 python bench.py > $D/bench.log 2>&1
   step bench $?
