@@ -95,8 +95,9 @@ def paired_oracle_run(img, cfg, seed):
 def test_oracle_only_discordance_rate():
     """The paired C2 gate's frozen null rate (tests/test_gpu_paired.py
     DISCORDANCE = 19/276): the float64 oracle and its float32-class build on
-    the seeds both committed targets hold end in different log Z modes (cut:
-    the common seeds' float64 median - 40 nats) in 19 of 276 runs, 10 : 9."""
+    the seeds both targets held when it was frozen (below 2000) end in
+    different log Z modes (cut: those seeds' float64 median - 40 nats) in 19
+    of 276 runs, 10 : 9."""
     import json
     import os
 
@@ -108,7 +109,9 @@ def test_oracle_only_discordance_rate():
             return {r["seed"]: r["logZ"] for r in json.load(f)["runs"]}
     a = logz("stats_c2_moderate_4096_k100_oracle.json")
     b = logz("stats_c2_moderate_4096_k100_oracle_f32.json")
-    common = sorted(set(a) & set(b))
+    # the frozen set: seeds below 2000 (runs added later, e.g. the round-6
+    # f32 / f64 pairs at seeds >= 10000, are supporting evidence only)
+    common = sorted(s for s in set(a) & set(b) if s < 2000)
     la, lb = np.array([a[s] for s in common]), np.array([b[s] for s in common])
     cut = np.median(la) - 40.0
     x, y = la < cut, lb < cut
