@@ -44,8 +44,9 @@ def count_posterior_compare(a_runs, b_runs, var_floor=None, nbins=11):
     # test of one law: under it both samples estimate the same per-bin
     # variance).  Reported beside the pre-registered statistic above: in a
     # rare bin where one sample happens to hold no mass (e.g. bin 10 of the
-    # C2 target: 16 of 2308 oracle runs carry ~0.1%), the unpooled SE is the
-    # other sample's alone and |z| ~ sqrt(its non-zero runs) whatever the laws
+    # C2 target: 36 of 2308 oracle runs carry a little), the unpooled SE is
+    # the other sample's alone and |z| grows with its non-zero runs whatever
+    # the laws
     vp = ((na - 1) * Ha.var(0, ddof=1) + (nb - 1) * Hb.var(0, ddof=1)) / max(na + nb - 2, 1)
     sp = np.sqrt(vp * (1.0 / na + 1.0 / nb))
     zp = np.where(sp > 0, d / np.where(sp > 0, sp, 1.0), np.where(d == 0, 0.0, np.inf))
