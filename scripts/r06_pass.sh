@@ -45,6 +45,7 @@ if has paired; then
   # every oracle run of the C2 target replayed on the GPU (tests/test_gpu_paired.py);
   # -s: every seed's line reaches the log as it is written
   SMCDET_PAIRED_ALL=1 SMCDET_PAIRED_NO_TWIN=${NO_TWIN:-1} SMCDET_PAIRED_CHUNKS=${CHUNKS:-48} \
+    SMCDET_PAIRED_PART=${PART:-} \
     SMCDET_PAIRED_OUT=$D/paired_all.json timeout -k 10 ${PAIRED_LIMIT:-3000} \
     python -u -m pytest tests/test_gpu_paired.py -s -q -p no:cacheprovider --timeout 600 \
     --timeout-method thread > $D/paired_all.log 2>&1

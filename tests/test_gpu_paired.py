@@ -69,6 +69,11 @@ def _target():
         doc = json.load(f)
     if os.environ.get("SMCDET_PAIRED_ALL") != "1":
         doc["runs"] = sorted(doc["runs"], key=lambda r: r["seed"])[:48]
+    elif os.environ.get("SMCDET_PAIRED_PART"):
+        # "k/P": the k-th of P interleaved parts of every run (one GPU call
+        # each; scripts/paired_combine.py pools the parts' per-run results)
+        k, P = (int(x) for x in os.environ["SMCDET_PAIRED_PART"].split("/"))
+        doc["runs"] = sorted(doc["runs"], key=lambda r: r["seed"])[k::P]
     return doc
 
 
