@@ -3,7 +3,10 @@
 These are small elementwise utilities kept for API compatibility
 (`DiscreteUniform` :5-19, `TruncatedDiagonalMVN` :22-58, `TruncatedPareto`
 :61-89).  They run as torch elementwise ops on whatever device their tensors
-live on.  The hot path does not call them: the MH kernel samples and scores
+live on.  Their formulas are the API (a user's code calls them), so they
+follow the reference line for line; tests/test_dropin_distributions.py pins
+them bit for bit to the reference's own outputs (tests/golden/distributions.npz).
+The hot path does not call them: the MH kernel samples and scores
 its truncated-normal proposals in-kernel (smcdet_amd/csrc/mh_kernel.hip) and
 the prior kernels evaluate the truncated Pareto density on device.
 """
@@ -75,9 +78,11 @@ class TruncatedPareto(Distribution):
         self.logpdf_norm_const = torch.tensor(
             math.log(a) + a * math.log(L) + a * math.log(U) - math.log(U ** a - L ** a))
 
-    def sample(self, shape=(), device=None):
+    def sample(self, shape=(), device=None, u=None):
+        """u: injected uniforms of `shape` (as TruncatedDiagonalMVN.sample's),
+        else torch.rand draws them."""
         device = device if device is not None else torch.get_default_device()
-        unif = torch.rand(tuple(shape), device=device)
+        unif = torch.rand(tuple(shape), device=device) if u is None else u.to(device)
         a, L, U = self.alpha.to(device), self.lower.to(device), self.upper.to(device)
         numerator = U ** a - unif * (U ** a) + unif * (L ** a)
         denominator = (L ** a) * (U ** a)
