@@ -13,6 +13,13 @@ interval of the relative difference -- "within 1%" is resolved when that
 interval lies inside +-1%.
 
     python scripts/c2_law.py [n_runs=8192] > profiles/r06/c2_law.json
+
+SMCDET_LAW_DUMP=<file.npz> also writes the GPU runs' per-run summaries
+(log Z, final ESS, iterations, pruned-count histogram, pruned flux), so the
+comparison can be recomputed on the CPU against a grown target without
+another GPU run:
+
+    python scripts/c2_law.py --recompute <file.npz> > profiles/r06/c2_law.json
 """
 import contextlib
 import io
@@ -27,15 +34,15 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-import bench  # noqa: E402
-from smcdet_amd.images import M71ImageModel  # noqa: E402
-from smcdet_amd.kernel import SingleComponentMH  # noqa: E402
-from smcdet_amd.prior import M71Prior  # noqa: E402
-from smcdet_amd.sampler import SMCsampler  # noqa: E402
 from tests._stats import count_posterior_compare, hist_var  # noqa: E402
 
 
 def gpu_runs(ref, n_runs, seed, chunk=2048):
+    import bench
+    from smcdet_amd.images import M71ImageModel
+    from smcdet_amd.kernel import SingleComponentMH
+    from smcdet_amd.prior import M71Prior
+    from smcdet_amd.sampler import SMCsampler
     dev = torch.device("cuda", 0)
     cfg = ref["config"]
     p, H, S, N, K = bench.M71, cfg["tile"], cfg["S"], cfg["N"], cfg["K"]
@@ -71,6 +78,7 @@ def gpu_runs(ref, n_runs, seed, chunk=2048):
                          "mean_total_flux_pruned": float(pflux[i])})
         del s
         torch.cuda.empty_cache()
+        print(f"{c0 + n} runs", file=sys.stderr, flush=True)  # progress
     return runs
 
 
@@ -87,18 +95,44 @@ def compare(ours, theirs, key):
             "diff_in_pooled_se": d / se if se > 0 else 0.0}
 
 
+def dump(runs, path, meta):
+    np.savez_compressed(
+        path, logZ=np.array([r["logZ"] for r in runs]),
+        final_ess=np.array([r["final_ess"] for r in runs]),
+        iters=np.array([r["iters"] for r in runs], dtype=np.int32),
+        pruned_hist=np.array([r["pruned_hist"] for r in runs], dtype=np.float64),
+        mean_total_flux_pruned=np.array([r["mean_total_flux_pruned"] for r in runs]),
+        meta=json.dumps(meta))
+
+
+def load(path):
+    z = np.load(path, allow_pickle=False)
+    runs = [{"logZ": float(a), "final_ess": float(b), "iters": int(c), "pruned_hist": h.tolist(),
+             "mean_total_flux_pruned": float(f)}
+            for a, b, c, h, f in zip(z["logZ"], z["final_ess"], z["iters"], z["pruned_hist"],
+                                     z["mean_total_flux_pruned"])]
+    return runs, json.loads(str(z["meta"]))
+
+
 def main():
-    n_runs = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
     g = os.path.join(ROOT, "tests", "golden")
     orc = json.load(open(os.path.join(g, "stats_c2_moderate_4096_k100_oracle.json")))
     ref = json.load(open(os.path.join(g, "stats_c2_moderate_4096_k100.json")))
-    t0 = time.perf_counter()
-    ours = gpu_runs(ref, n_runs, seed=90210)
-    out = {"config": "C2: 32x32 M71 tile (stats_c2_moderate_4096_k100 image), S=10, N=4096, "
-                     "K=100, systematic, rho=0.5; GPU runs = one launch grid of copies, "
-                     "independent stopping",
-           "gpu_runs": len(ours), "gpu_wall_s": time.perf_counter() - t0,
-           "library": __import__("smcdet_amd._hip", fromlist=["x"]).version()}
+    if len(sys.argv) > 2 and sys.argv[1] == "--recompute":
+        ours, out = load(sys.argv[2])
+        out["recomputed_from"] = os.path.basename(sys.argv[2])
+    else:
+        n_runs = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+        t0 = time.perf_counter()
+        ours = gpu_runs(ref, n_runs, seed=90210)
+        out = {"config": "C2: 32x32 M71 tile (stats_c2_moderate_4096_k100 image), S=10, N=4096, "
+                         "K=100, systematic, rho=0.5; GPU runs = one launch grid of copies, "
+                         "independent stopping",
+               "gpu_runs": len(ours), "gpu_wall_s": time.perf_counter() - t0,
+               "library": __import__("smcdet_amd._hip", fromlist=["x"]).version()}
+        if os.environ.get("SMCDET_LAW_DUMP"):
+            dump(ours, os.environ["SMCDET_LAW_DUMP"], out)
+    out["oracle_runs"] = len(orc["runs"])
     cut = float(np.median([r["logZ"] for r in orc["runs"]]) - 40.0)
     for name, tgt in (("vs_oracle", orc["runs"]), ("vs_reference", ref["runs"])):
         res = {k: compare(ours, tgt, k) for k in ("logZ", "final_ess", "iters")}
